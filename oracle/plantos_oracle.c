@@ -1,0 +1,776 @@
+/*
+ * plantos_oracle.c -- CPU restatement of PlantOSEnv.step/reset.
+ *
+ * TEST INFRASTRUCTURE ONLY: the parity checker for the HIP hot path and the CPU
+ * baseline timed by bench.py.  Nothing in rl-env_amd/ links or calls this file.
+ *
+ * Each function cites the reference line(s) it restates.  Pinned against the
+ * reference's own outputs in tests/golden/ (tools/gen_golden.py) by
+ * tests/test_oracle_golden.py.
+ */
+#include "plantos_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+enum { EMPTY = 0, OBST = 1, HYD = 2, THIRSTY = 3 };
+
+void po_default_config(po_config* c, int G, int P, int O, int R, int C) {
+    memset(c, 0, sizeof(*c));
+    c->grid_size = G;
+    c->num_plants = P;
+    c->num_obstacles = O;
+    c->lidar_range = R;
+    c->lidar_channels = C;
+    c->max_steps = 1000;              /* plantos_env.py:120 */
+    c->thirsty_plant_prob = 0.7;      /* plantos_env.py:26 */
+    c->r_goal = 20;                   /* plantos_env.py:76-83 (DQN preset, the active one) */
+    c->r_mistake = -10;
+    c->r_invalid = -5;
+    c->r_water_empty = -5;
+    c->r_step = -0.1;
+    c->r_exploration = 10;
+    c->r_revisit = -1;
+    c->r_complete = 50;
+}
+
+/* plantos_env.py:55-57: lidar_channels*5 + 2 + 25 */
+int po_obs_dim(const po_config* c) { return c->lidar_channels * 5 + 2 + 25; }
+
+/* plantos_env.py:260-267: angle = (2*pi*i)/C; dx = int(r*cos(angle)); dy = int(r*sin(angle)).
+ * Python evaluates 2*math.pi*i left to right, then divides; int() truncates toward 0. */
+void po_lidar_table(int C, int R, int32_t* dx, int32_t* dy) {
+    const double pi = 3.141592653589793; /* math.pi */
+    for (int i = 0; i < C; ++i) {
+        double angle = ((2.0 * pi) * (double)i) / (double)C;
+        for (int r = 1; r <= R; ++r) {
+            dx[i * R + r - 1] = (int32_t)((double)r * cos(angle));
+            dy[i * R + r - 1] = (int32_t)((double)r * sin(angle));
+        }
+    }
+}
+
+typedef struct {
+    int32_t* dx;
+    int32_t* dy;
+} lidar_tab;
+
+static lidar_tab tab_new(const po_config* c) {
+    lidar_tab t;
+    size_t n = (size_t)c->lidar_channels * (size_t)c->lidar_range;
+    t.dx = (int32_t*)malloc(sizeof(int32_t) * (n ? n : 1));
+    t.dy = (int32_t*)malloc(sizeof(int32_t) * (n ? n : 1));
+    po_lidar_table(c->lidar_channels, c->lidar_range, t.dx, t.dy);
+    return t;
+}
+static void tab_free(lidar_tab* t) {
+    free(t->dx);
+    free(t->dy);
+}
+
+/* _get_lidar_obs, plantos_env.py:251-315 */
+static void obs_with(const po_config* c, const lidar_tab* t, const uint8_t* cells, const int32_t* visits,
+                     const int32_t* scal, float* obs) {
+    const int G = c->grid_size, R = c->lidar_range, C = c->lidar_channels;
+    const int D = po_obs_dim(c);
+    const int x = scal[PO_S_X], y = scal[PO_S_Y];
+    memset(obs, 0, sizeof(float) * (size_t)D);
+    for (int i = 0; i < C; ++i) {                                  /* :260 */
+        int dist = R, ent = EMPTY;                                 /* :262-263 */
+        for (int r = 1; r <= R; ++r) {                             /* :265 */
+            int cx = x + t->dx[i * R + r - 1], cy = y + t->dy[i * R + r - 1];
+            if (!(0 <= cx && cx < G && 0 <= cy && cy < G)) {       /* :271-274 wall == obstacle */
+                dist = r;
+                ent = OBST;
+                break;
+            }
+            int code = cells[cx * G + cy];
+            if (code == OBST) {                                    /* :277-280 */
+                dist = r;
+                ent = OBST;
+                break;
+            } else if (code == HYD || code == THIRSTY) {           /* :281-284 */
+                dist = r;
+                ent = code; /* ENTITY_PLANT_HYDRATED=2 / ENTITY_PLANT_THIRSTY=3 */
+                break;
+            }
+        }
+        obs[5 * i] = (float)((double)dist / (double)R);            /* :288 */
+        obs[5 * i + 1 + ent] = 1.0f;                               /* :290-292 */
+    }
+    obs[5 * C] = (float)((double)x / (double)G);                   /* :295 */
+    obs[5 * C + 1] = (float)((double)y / (double)G);               /* :296 */
+    for (int lx = 0; lx < 5; ++lx) {                               /* :302-311 */
+        for (int ly = 0; ly < 5; ++ly) {
+            int gx = x + (lx - 2), gy = y + (ly - 2);
+            float v;
+            if (0 <= gx && gx < G && 0 <= gy && gy < G) {
+                int32_t vc = visits[gx * G + gy];
+                v = (float)((double)(vc < 10 ? vc : 10) / 10.0);   /* min(v,10)/10.0 */
+            } else {
+                v = 1.0f;
+            }
+            obs[5 * C + 2 + lx * 5 + ly] = v;
+        }
+    }
+}
+
+void po_obs(const po_config* c, const uint8_t* cells, const int32_t* visits, const int32_t* scal, float* obs) {
+    lidar_tab t = tab_new(c);
+    obs_with(c, &t, cells, visits, scal, obs);
+    tab_free(&t);
+}
+
+/* _get_info, plantos_env.py:317-336 */
+void po_info(const po_config* c, const uint8_t* cells, const int8_t* explored, int32_t* out) {
+    const int GG = c->grid_size * c->grid_size;
+    int th = 0, hy = 0, ex = 0, ob = 0;
+    for (int k = 0; k < GG; ++k) {
+        th += cells[k] == THIRSTY;
+        hy += cells[k] == HYD;
+        ob += cells[k] == OBST;
+        ex += explored[k] > 0;                                     /* np.sum(explored_map > 0), :320 */
+    }
+    out[0] = th;
+    out[1] = hy;
+    out[2] = th + hy;
+    out[3] = ex;
+    out[4] = GG - ob;                                              /* :321 */
+}
+
+/* step, plantos_env.py:160-183 (+ _handle_movement 185-211, _handle_watering of the
+ * fork gradio-app/plantos_env_new.py:236-245; the root's None return is flagged). */
+static void step_with(const po_config* c, const lidar_tab* t, uint8_t* cells, int32_t* visits, int8_t* explored,
+                      int32_t* scal, int64_t action, float* obs, double* reward, uint8_t* term,
+                      uint8_t* trunc) {
+    static const int DIRS[4][2] = {{-1, 0}, {0, 1}, {1, 0}, {0, -1}}; /* :186 N,E,S,W */
+    const int G = c->grid_size;
+    scal[PO_S_STEP] += 1;                                          /* :162 */
+    double rew = c->r_step;                                        /* :164 */
+    if (action < 4) {                                              /* :166 */
+        int64_t a = action;
+        if (a < 0) a += 4;                                         /* Python negative list index */
+        if (a < 0) {
+            scal[PO_S_POISONED] |= 2;                              /* reference: IndexError */
+        } else {
+            int x = scal[PO_S_X], y = scal[PO_S_Y];
+            int nx = x + DIRS[a][0], ny = y + DIRS[a][1];          /* :187-190 */
+            if (0 <= nx && nx < G && 0 <= ny && ny < G && cells[nx * G + ny] != OBST) { /* :193-195 */
+                int was_never = visits[nx * G + ny] == 0;          /* :197 */
+                explored[x * G + y] = 1;                           /* :198 */
+                scal[PO_S_X] = nx;                                 /* :199 */
+                scal[PO_S_Y] = ny;
+                explored[nx * G + ny] = 2;                         /* :200 */
+                visits[nx * G + ny] += 1;                          /* :203 */
+                rew += was_never ? c->r_exploration : c->r_revisit; /* :204-207 */
+            } else {
+                scal[PO_S_COLLIDED] = 1;                           /* :209 */
+                scal[PO_S_COLL] += 1;                              /* :210 */
+                rew += c->r_invalid;                               /* :211 */
+            }
+        }
+    } else {
+        int k = scal[PO_S_X] * G + scal[PO_S_Y];
+        if (cells[k] == THIRSTY) {                                 /* fork :237-240 */
+            cells[k] = HYD;
+            rew += c->r_goal;
+        } else if (cells[k] == HYD) {                              /* fork :241-242 (root: returns None) */
+            rew += c->r_mistake;
+            scal[PO_S_POISONED] |= 1;
+        } else {
+            rew += c->r_water_empty;                               /* :221-222 */
+        }
+    }
+    obs_with(c, t, cells, visits, scal, obs);                      /* :173 */
+    int32_t info[5];
+    po_info(c, cells, explored, info);                             /* :174 */
+    double pct = ((double)info[3] / (double)info[4]) * 100.0;      /* :331 */
+    *term = pct >= 100.0;                                          /* :176, 244-246 */
+    *trunc = scal[PO_S_STEP] >= c->max_steps;                      /* :177 */
+    if (pct >= 100.0 && !scal[PO_S_BONUS]) {                       /* :179-181 */
+        rew += c->r_complete;
+        scal[PO_S_BONUS] = 1;
+    }
+    *reward = rew;
+}
+
+void po_step(const po_config* c, uint8_t* cells, int32_t* visits, int8_t* explored, int32_t* scal,
+             int64_t action, float* obs, double* reward, uint8_t* terminated, uint8_t* truncated) {
+    lidar_tab t = tab_new(c);
+    step_with(c, &t, cells, visits, explored, scal, action, obs, reward, terminated, truncated);
+    tab_free(&t);
+}
+
+void po_step_batch(const po_config* c, int64_t n, uint8_t* cells, int32_t* visits, int8_t* explored,
+                   int32_t* scal, const int64_t* actions, float* obs, double* reward,
+                   uint8_t* terminated, uint8_t* truncated) {
+    const int64_t GG = (int64_t)c->grid_size * c->grid_size;
+    const int D = po_obs_dim(c);
+    lidar_tab t = tab_new(c);
+    for (int64_t e = 0; e < n; ++e)
+        step_with(c, &t, cells + e * GG, visits + e * GG, explored + e * GG, scal + e * PO_NSCAL, actions[e],
+                  obs + e * D, reward + e, terminated + e, truncated + e);
+    tab_free(&t);
+}
+
+/* ====================================================================== RNGs */
+/* CPython Modules/_randommodule.c: MT19937 (init_genrand / init_by_array / genrand_uint32). */
+static void mt_init_genrand(po_mt* m, uint32_t s) {
+    m->mt[0] = s;
+    for (int i = 1; i < 624; ++i)
+        m->mt[i] = 1812433253u * (m->mt[i - 1] ^ (m->mt[i - 1] >> 30)) + (uint32_t)i;
+    m->index = 624;
+}
+
+static void mt_init_by_array(po_mt* m, const uint32_t* key, int len) {
+    mt_init_genrand(m, 19650218u);
+    int i = 1, j = 0;
+    int k = 624 > len ? 624 : len;
+    for (; k; --k) {
+        m->mt[i] = (m->mt[i] ^ ((m->mt[i - 1] ^ (m->mt[i - 1] >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
+        ++i;
+        ++j;
+        if (i >= 624) {
+            m->mt[0] = m->mt[623];
+            i = 1;
+        }
+        if (j >= len) j = 0;
+    }
+    for (k = 623; k; --k) {
+        m->mt[i] = (m->mt[i] ^ ((m->mt[i - 1] ^ (m->mt[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
+        ++i;
+        if (i >= 624) {
+            m->mt[0] = m->mt[623];
+            i = 1;
+        }
+    }
+    m->mt[0] = 0x80000000u;
+    m->index = 624;
+}
+
+/* random.seed(n) for a non-negative int n: key = 32-bit chunks of n, little-endian. */
+void po_mt_seed(po_mt* m, uint64_t seed) {
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    mt_init_by_array(m, key, key[1] ? 2 : 1);
+}
+
+uint32_t po_mt_u32(po_mt* m) {
+    static const uint32_t mag01[2] = {0u, 0x9908b0dfu};
+    uint32_t y;
+    if (m->index >= 624) {
+        int kk;
+        for (kk = 0; kk < 624 - 397; ++kk) {
+            y = (m->mt[kk] & 0x80000000u) | (m->mt[kk + 1] & 0x7fffffffu);
+            m->mt[kk] = m->mt[kk + 397] ^ (y >> 1) ^ mag01[y & 1u];
+        }
+        for (; kk < 623; ++kk) {
+            y = (m->mt[kk] & 0x80000000u) | (m->mt[kk + 1] & 0x7fffffffu);
+            m->mt[kk] = m->mt[kk + (397 - 624)] ^ (y >> 1) ^ mag01[y & 1u];
+        }
+        y = (m->mt[623] & 0x80000000u) | (m->mt[0] & 0x7fffffffu);
+        m->mt[623] = m->mt[396] ^ (y >> 1) ^ mag01[y & 1u];
+        m->index = 0;
+    }
+    y = m->mt[m->index++];
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+
+/* Philox4x32-10 (Salmon et al., SC'11), the device-rng stream. */
+void po_philox4x32(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int round = 0; round < 10; ++round) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        c0 = hi1 ^ c1 ^ k0;
+        c1 = lo1;
+        c2 = hi0 ^ c3 ^ k1;
+        c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0;
+    out[1] = c1;
+    out[2] = c2;
+    out[3] = c3;
+}
+
+#define PO_DOMAIN_RESET 0x50455352u  /* "RSEP" */
+#define PO_DOMAIN_ACTION 0x4E544341u /* "ACTN" */
+
+int32_t po_synth_action(uint64_t seed, uint32_t env_id, uint32_t t) {
+    uint32_t ctr[4] = {t, env_id, 0u, PO_DOMAIN_ACTION};
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t o[4];
+    po_philox4x32(ctr, key, o);
+    return (int32_t)(o[0] % 5u);
+}
+
+/* A u32 source: either CPython's MT stream or a Philox counter stream. */
+typedef struct {
+    po_mt* mt;
+    uint32_t key[2];
+    uint32_t ctr[4];
+    uint32_t buf[4];
+    int pos;
+} u32src;
+
+static uint32_t src_u32(u32src* s) {
+    if (s->mt) return po_mt_u32(s->mt);
+    if (s->pos == 4) {
+        po_philox4x32(s->ctr, s->key, s->buf);
+        s->ctr[0] += 1u;
+        s->pos = 0;
+    }
+    return s->buf[s->pos++];
+}
+
+static int bit_length(uint32_t n) {
+    int k = 0;
+    while (n) {
+        ++k;
+        n >>= 1;
+    }
+    return k;
+}
+
+/* random.py:239-248 _randbelow_with_getrandbits; getrandbits(k<=32) = u32 >> (32-k). */
+static uint32_t randbelow(u32src* s, uint32_t n) {
+    if (!n) return 0;
+    int k = bit_length(n);
+    uint32_t r = src_u32(s) >> (32 - k);
+    while (r >= n) r = src_u32(s) >> (32 - k);
+    return r;
+}
+
+/* random.random(): (a*2^26 + b) / 2^53 with a = u32>>5, b = u32>>6. */
+static double random53(u32src* s) {
+    uint32_t a = src_u32(s) >> 5, b = src_u32(s) >> 6;
+    return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
+}
+
+/* ======================================= CPython 3.10 set emulation (setobject.c) */
+#define PS_NULL (-1)
+#define PS_DUMMY (-2)
+#define PS_MINSIZE 8
+#define PS_LINEAR_PROBES 9
+#define PS_PERTURB_SHIFT 5
+
+typedef struct {
+    int64_t* hash;
+    int32_t* key; /* cell id x*G+y, or PS_NULL / PS_DUMMY */
+    uint64_t mask;
+    int64_t fill, used;
+} pyset;
+
+/* tuplehash for (x, y), Objects/tupleobject.c (xxHash-based, 64-bit); hash(small int) = int. */
+static int64_t tuple2_hash(int64_t a, int64_t b) {
+    const uint64_t P1 = 11400714785074694791ULL, P2 = 14029467366897019727ULL, P5 = 2870177450012600261ULL;
+    uint64_t acc = P5;
+    uint64_t lanes[2] = {(uint64_t)a, (uint64_t)b};
+    for (int i = 0; i < 2; ++i) {
+        acc += lanes[i] * P2;
+        acc = (acc << 31) | (acc >> 33);
+        acc *= P1;
+    }
+    acc += (uint64_t)2 ^ (P5 ^ 3527539UL);
+    if (acc == (uint64_t)-1) return 1546275796;
+    return (int64_t)acc;
+}
+
+static void ps_alloc(pyset* s, uint64_t size) {
+    s->hash = (int64_t*)calloc(size, sizeof(int64_t));
+    s->key = (int32_t*)malloc(size * sizeof(int32_t));
+    for (uint64_t i = 0; i < size; ++i) s->key[i] = PS_NULL;
+    s->mask = size - 1;
+    s->fill = s->used = 0;
+}
+static void ps_free(pyset* s) {
+    free(s->hash);
+    free(s->key);
+}
+
+static void ps_insert_clean(int64_t* H, int32_t* K, uint64_t mask, int32_t key, int64_t hash) {
+    uint64_t perturb = (uint64_t)hash;
+    uint64_t i = (uint64_t)hash & mask;
+    for (;;) {
+        if (K[i] == PS_NULL) goto found;
+        if (i + PS_LINEAR_PROBES <= mask) {
+            for (uint64_t j = 1; j <= PS_LINEAR_PROBES; ++j) {
+                if (K[i + j] == PS_NULL) {
+                    i = i + j;
+                    goto found;
+                }
+            }
+        }
+        perturb >>= PS_PERTURB_SHIFT;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+found:
+    K[i] = key;
+    H[i] = hash;
+}
+
+/* set_table_resize */
+static void ps_resize(pyset* s, int64_t minused) {
+    uint64_t newsize = PS_MINSIZE;
+    while (newsize <= (uint64_t)minused) newsize <<= 1;
+    int64_t* oh = s->hash;
+    int32_t* ok = s->key;
+    uint64_t omask = s->mask;
+    ps_alloc(s, newsize);
+    int64_t used = 0;
+    for (uint64_t i = 0; i <= omask; ++i) {
+        if (ok[i] != PS_NULL && ok[i] != PS_DUMMY) {
+            ps_insert_clean(s->hash, s->key, s->mask, ok[i], oh[i]);
+            ++used;
+        }
+    }
+    s->fill = s->used = used;
+    free(oh);
+    free(ok);
+}
+
+/* set_add_entry */
+static void ps_add(pyset* s, int32_t key, int64_t hash) {
+    uint64_t mask = s->mask;
+    uint64_t i = (uint64_t)hash & mask;
+    uint64_t perturb = (uint64_t)hash;
+    int64_t freeslot = -1;
+    for (;;) {
+        uint64_t e = i;
+        int probes = (i + PS_LINEAR_PROBES <= mask) ? PS_LINEAR_PROBES : 0;
+        do {
+            if (s->hash[e] == 0 && s->key[e] == PS_NULL) goto unused_or_dummy;
+            if (s->hash[e] == hash && s->key[e] != PS_DUMMY) {
+                if (s->key[e] == key) return; /* found active */
+            } else if (s->hash[e] == -1 && s->key[e] == PS_DUMMY) {
+                if (freeslot < 0) freeslot = (int64_t)e;
+            }
+            ++e;
+        } while (probes--);
+        perturb >>= PS_PERTURB_SHIFT;
+        i = (i * 5 + 1 + perturb) & mask;
+        continue;
+    unused_or_dummy:
+        if (freeslot >= 0) {
+            s->used++;
+            s->key[freeslot] = key;
+            s->hash[freeslot] = hash;
+            return;
+        }
+        s->fill++;
+        s->used++;
+        s->key[e] = key;
+        s->hash[e] = hash;
+        if ((uint64_t)s->fill * 5 < mask * 3) return;
+        ps_resize(s, s->used > 50000 ? s->used * 2 : s->used * 4);
+        return;
+    }
+}
+
+/* set_lookkey: index of the active entry holding key, or -1 */
+static int64_t ps_find(const pyset* s, int32_t key, int64_t hash) {
+    uint64_t mask = s->mask;
+    uint64_t i = (uint64_t)hash & mask;
+    uint64_t perturb = (uint64_t)hash;
+    for (;;) {
+        uint64_t e = i;
+        int probes = (i + PS_LINEAR_PROBES <= mask) ? PS_LINEAR_PROBES : 0;
+        do {
+            if (s->hash[e] == 0 && s->key[e] == PS_NULL) return -1;
+            if (s->hash[e] == hash && s->key[e] == key) return (int64_t)e;
+            ++e;
+        } while (probes--);
+        perturb >>= PS_PERTURB_SHIFT;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+}
+
+static void ps_discard(pyset* s, int32_t key, int64_t hash) {
+    int64_t e = ps_find(s, key, hash);
+    if (e < 0) return;
+    s->key[e] = PS_DUMMY;
+    s->hash[e] = -1;
+    s->used--;
+}
+
+/* set_difference_update_internal(so, other_set) given other's members */
+static void ps_difference_update(pyset* s, const int32_t* keys, const int64_t* hashes, int n) {
+    for (int k = 0; k < n; ++k) ps_discard(s, keys[k], hashes[k]);
+    if ((uint64_t)(s->fill - s->used) <= s->mask / 4) return;
+    ps_resize(s, s->used > 50000 ? s->used * 2 : s->used * 4);
+}
+
+/* set_merge into an EMPTY new set (the set_copy path) */
+static void ps_copy(const pyset* o, pyset* s) {
+    ps_alloc(s, PS_MINSIZE);
+    if (o->used == 0) return;
+    if ((uint64_t)(s->fill + o->used) * 5 >= s->mask * 3) {
+        ps_free(s);
+        uint64_t newsize = PS_MINSIZE;
+        while (newsize <= (uint64_t)(o->used * 2)) newsize <<= 1;
+        ps_alloc(s, newsize);
+    }
+    if (s->mask == o->mask && o->fill == o->used) {
+        for (uint64_t i = 0; i <= o->mask; ++i) {
+            s->key[i] = o->key[i];
+            s->hash[i] = o->hash[i];
+        }
+        s->fill = o->fill;
+        s->used = o->used;
+        return;
+    }
+    for (uint64_t i = 0; i <= o->mask; ++i)
+        if (o->key[i] != PS_NULL && o->key[i] != PS_DUMMY) ps_insert_clean(s->hash, s->key, s->mask, o->key[i], o->hash[i]);
+    s->fill = s->used = o->used;
+}
+
+static int ps_list(const pyset* s, int32_t* out) {
+    int n = 0;
+    for (uint64_t i = 0; i <= s->mask; ++i)
+        if (s->key[i] != PS_NULL && s->key[i] != PS_DUMMY) out[n++] = s->key[i];
+    return n;
+}
+
+/* available_positions = set((x,y) for x in range(G) for y in range(G)) - self.obstacles
+ * (plantos_env.py:356-358): set_difference() in Objects/setobject.c. */
+static void ps_free_cells(int G, const uint8_t* obst, pyset* out) {
+    pyset full;
+    ps_alloc(&full, PS_MINSIZE);
+    for (int x = 0; x < G; ++x)
+        for (int y = 0; y < G; ++y) ps_add(&full, x * G + y, tuple2_hash(x, y));
+    int n_obst = 0;
+    for (int k = 0; k < G * G; ++k) n_obst += obst[k] != 0;
+    if ((full.used >> 2) > n_obst) {
+        /* set_copy_and_difference */
+        ps_copy(&full, out);
+        int32_t* keys = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n_obst + 1));
+        int64_t* hs = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n_obst + 1));
+        int m = 0;
+        for (int k = 0; k < G * G; ++k)
+            if (obst[k]) {
+                keys[m] = k;
+                hs[m] = tuple2_hash(k / G, k % G);
+                ++m;
+            }
+        ps_difference_update(out, keys, hs, m);
+        free(keys);
+        free(hs);
+    } else {
+        ps_alloc(out, PS_MINSIZE);
+        for (uint64_t i = 0; i <= full.mask; ++i) {
+            int32_t k = full.key[i];
+            if (k == PS_NULL || k == PS_DUMMY) continue;
+            if (!obst[k]) ps_add(out, k, full.hash[i]);
+        }
+    }
+    ps_free(&full);
+}
+
+int po_pyset_free_list(int G, const uint8_t* obstacle_mask, int32_t* out) {
+    pyset s;
+    ps_free_cells(G, obstacle_mask, &s);
+    int n = ps_list(&s, out);
+    ps_free(&s);
+    return n;
+}
+
+/* ================================================================ map generation */
+/* _generate_map, plantos_env.py:338-372; `cpython` selects list order + sample algorithm. */
+static int generate_map(const po_config* c, u32src* src, int cpython, uint8_t* cells, int* rx, int* ry) {
+    const int G = c->grid_size, P = c->num_plants;
+    const int GG = G * G;
+    uint8_t* obst = (uint8_t*)calloc((size_t)GG, 1);
+    const int clusters = c->num_obstacles / 3;                     /* :341 */
+    for (int q = 0; q < clusters; ++q) {                           /* :343 */
+        int cx = 2 + (int)randbelow(src, (uint32_t)(G - 4));       /* randint(2, G-3) :344 */
+        int cy = 2 + (int)randbelow(src, (uint32_t)(G - 4));       /* :345 */
+        int size = 2 + (int)randbelow(src, 2u);                    /* choice([2, 3]) :347 */
+        for (int dx = 0; dx < size; ++dx)
+            for (int dy = 0; dy < size; ++dy) {
+                int ox = cx + dx - size / 2, oy = cy + dy - size / 2; /* :350-351 */
+                if (0 <= ox && ox < G && 0 <= oy && oy < G) obst[ox * G + oy] = 1; /* :353-354 */
+            }
+    }
+    int32_t* list = (int32_t*)malloc(sizeof(int32_t) * (size_t)GG);
+    pyset avail;
+    int n;
+    if (cpython) {
+        ps_free_cells(G, obst, &avail);                            /* :356-358 */
+        n = ps_list(&avail, list);
+    } else {
+        n = 0;
+        for (int k = 0; k < GG; ++k)
+            if (!obst[k]) list[n++] = k;                           /* row-major candidate list */
+    }
+    if (n < P + 1) {                                               /* :360-364 ValueError */
+        if (cpython) ps_free(&avail);
+        free(list);
+        free(obst);
+        return -1;
+    }
+    /* random.sample(list(available_positions), P), random.py:sample (3.10) :366 */
+    int32_t* picks = (int32_t*)malloc(sizeof(int32_t) * (size_t)(P + 1));
+    int setsize = 21;
+    if (P > 5) setsize += (int)pow(4.0, ceil(log((double)(P * 3)) / log(4.0)));
+    if (cpython && n <= setsize) {
+        int32_t* pool = (int32_t*)malloc(sizeof(int32_t) * (size_t)n);
+        memcpy(pool, list, sizeof(int32_t) * (size_t)n);
+        for (int i = 0; i < P; ++i) {
+            int j = (int)randbelow(src, (uint32_t)(n - i));
+            picks[i] = pool[j];
+            pool[j] = pool[n - i - 1];
+        }
+        free(pool);
+    } else {
+        uint8_t* selected = (uint8_t*)calloc((size_t)n, 1);
+        for (int i = 0; i < P; ++i) {
+            int j = (int)randbelow(src, (uint32_t)n);
+            while (selected[j]) j = (int)randbelow(src, (uint32_t)n);
+            selected[j] = 1;
+            picks[i] = list[j];
+        }
+        free(selected);
+    }
+    memset(cells, EMPTY, (size_t)GG);
+    for (int k = 0; k < GG; ++k)
+        if (obst[k]) cells[k] = OBST;
+    for (int i = 0; i < P; ++i) {                                  /* :367-369 */
+        int thirsty = random53(src) < c->thirsty_plant_prob;
+        cells[picks[i]] = thirsty ? THIRSTY : HYD;
+    }
+    /* available_positions -= set(plant_positions); choice(list(...))  :370-372 */
+    if (cpython) {
+        int64_t* hs = (int64_t*)malloc(sizeof(int64_t) * (size_t)(P + 1));
+        for (int i = 0; i < P; ++i) hs[i] = tuple2_hash(picks[i] / G, picks[i] % G);
+        ps_difference_update(&avail, picks, hs, P);
+        free(hs);
+        n = ps_list(&avail, list);
+        ps_free(&avail);
+    } else {
+        int m = 0;
+        for (int k = 0; k < GG; ++k)
+            if (!obst[k] && cells[k] == EMPTY) list[m++] = k;
+        n = m;
+    }
+    int r = list[randbelow(src, (uint32_t)n)];
+    *rx = r / G;
+    *ry = r % G;
+    free(picks);
+    free(list);
+    free(obst);
+    return 0;
+}
+
+/* reset(), plantos_env.py:125-158 (+ _initialize_exploration 224-238) */
+static int reset_common(const po_config* c, u32src* src, int cpython, uint8_t* cells, int32_t* visits,
+                        int8_t* explored, int32_t* scal) {
+    const int G = c->grid_size;
+    int rx = 0, ry = 0;
+    if (generate_map(c, src, cpython, cells, &rx, &ry) != 0) return -1;
+    memset(visits, 0, sizeof(int32_t) * (size_t)(G * G));
+    memset(explored, 0, (size_t)(G * G));
+    explored[rx * G + ry] = 2;                                     /* :236 */
+    visits[rx * G + ry] = 1;                                       /* :146-147 */
+    scal[PO_S_X] = rx;
+    scal[PO_S_Y] = ry;
+    scal[PO_S_STEP] = 0;                                           /* :130-133 */
+    scal[PO_S_COLL] = 0;
+    scal[PO_S_COLLIDED] = 0;
+    scal[PO_S_BONUS] = 0;
+    scal[PO_S_POISONED] = 0;
+    return 0;
+}
+
+int po_reset_cpython(const po_config* c, po_mt* mt, uint8_t* cells, int32_t* visits, int8_t* explored,
+                     int32_t* scal) {
+    u32src s;
+    memset(&s, 0, sizeof(s));
+    s.mt = mt;
+    int rc = reset_common(c, &s, 1, cells, visits, explored, scal);
+    scal[PO_S_EPISODE] += 1;
+    return rc;
+}
+
+int po_reset_philox(const po_config* c, uint64_t seed, uint32_t env_id, uint32_t episode, uint8_t* cells,
+                    int32_t* visits, int8_t* explored, int32_t* scal) {
+    u32src s;
+    memset(&s, 0, sizeof(s));
+    s.key[0] = (uint32_t)seed;
+    s.key[1] = (uint32_t)(seed >> 32);
+    s.ctr[0] = 0;
+    s.ctr[1] = env_id;
+    s.ctr[2] = episode;
+    s.ctr[3] = PO_DOMAIN_RESET;
+    s.pos = 4;
+    int rc = reset_common(c, &s, 0, cells, visits, explored, scal);
+    scal[PO_S_EPISODE] = (int32_t)(episode + 1u);
+    return rc;
+}
+
+/* ================================================================ CPU baseline */
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+double po_bench(const po_config* c, int64_t n_envs, int64_t steps, uint64_t seed, int threads, double* seconds) {
+    const int64_t GG = (int64_t)c->grid_size * c->grid_size;
+    const int D = po_obs_dim(c);
+    uint8_t* cells = (uint8_t*)malloc((size_t)(n_envs * GG));
+    int32_t* visits = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n_envs * GG));
+    int8_t* explored = (int8_t*)malloc((size_t)(n_envs * GG));
+    int32_t* scal = (int32_t*)calloc((size_t)(n_envs * PO_NSCAL), sizeof(int32_t));
+    float* obs = (float*)malloc(sizeof(float) * (size_t)(n_envs * D));
+    double* rew = (double*)malloc(sizeof(double) * (size_t)n_envs);
+    uint8_t* te = (uint8_t*)malloc((size_t)n_envs);
+    uint8_t* tr = (uint8_t*)malloc((size_t)n_envs);
+    lidar_tab t = tab_new(c);
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#else
+    (void)threads;
+#endif
+#pragma omp parallel for schedule(static)
+    for (int64_t e = 0; e < n_envs; ++e)
+        po_reset_philox(c, seed, (uint32_t)e, 0, cells + e * GG, visits + e * GG, explored + e * GG,
+                        scal + e * PO_NSCAL);
+    double checksum = 0.0;
+    double t0 = now_s();
+#pragma omp parallel for schedule(static) reduction(+ : checksum)
+    for (int64_t e = 0; e < n_envs; ++e) {
+        for (int64_t s = 0; s < steps; ++s) {
+            int64_t a = po_synth_action(seed, (uint32_t)e, (uint32_t)s);
+            step_with(c, &t, cells + e * GG, visits + e * GG, explored + e * GG, scal + e * PO_NSCAL, a,
+                      obs + e * D, rew + e, te + e, tr + e);
+            checksum += rew[e];
+            if (te[e] || tr[e])
+                po_reset_philox(c, seed, (uint32_t)e, (uint32_t)scal[e * PO_NSCAL + PO_S_EPISODE], cells + e * GG,
+                                visits + e * GG, explored + e * GG, scal + e * PO_NSCAL);
+        }
+    }
+    *seconds = now_s() - t0;
+    tab_free(&t);
+    free(cells);
+    free(visits);
+    free(explored);
+    free(scal);
+    free(obs);
+    free(rew);
+    free(te);
+    free(tr);
+    return checksum;
+}

@@ -1,0 +1,21 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG_ROOT = os.path.join(REPO, "rl-env_amd")
+for p in (REPO, PKG_ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through the HIP C-ABI)")
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    return GOLDEN

@@ -1,0 +1,2 @@
+"""Viewer stand-in (rendering is out of scope)."""
+PlantOS3DViewer = None
