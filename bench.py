@@ -1,0 +1,170 @@
+#!/usr/bin/env python3
+"""Benchmark of the batched PlantOSEnv step (BASELINE.json headline).
+
+A "step" = one pe_step launch over the whole batch: every env consumes one
+action and materializes obs f32[5C+27], reward f32, terminated u8, truncated u8
+in HBM, auto-resetting (device-rng map generation) when done.  Inputs are
+resident in HBM before the timed region; actions come from a pre-generated
+device buffer of synthetic actions philox(seed, env, t) % 5 (4 B read per env-step).
+
+  python bench.py [--gpus N --steps K --warmup W --envs E --grid G --rays C --range R]
+
+N>1: one process per GPU (torch.distributed.run); each rank owns a disjoint
+shard of E envs (global ids rank*E ...), no collective on the data path
+("scaling": "weak"); barrier + max-over-ranks timing.  --gather adds the
+host-boundary RCCL gather of (obs, reward, done) to rank 0 every step.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "rl-env_amd"))
+
+import torch  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+METRIC = "env-steps/sec at 64k parallel 20×20 envs; achieved HBM GB/s vs roofline"
+
+
+def algorithmic_bytes(C, R):
+    """B = B_io + B_state per env-step."""
+    b_io = 4 + 4 * (5 * C + 27) + 4 + 2
+    b_state = 8 + 50 + 2 + C * R + 16
+    return b_io + b_state
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=2000)
+    p.add_argument("--warmup", type=int, default=200)
+    p.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    p.add_argument("--grid", type=int, default=20)
+    p.add_argument("--plants", type=int, default=None)
+    p.add_argument("--obstacles", type=int, default=None)
+    p.add_argument("--rays", type=int, default=16)
+    p.add_argument("--range", type=int, default=6)
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--action-steps", type=int, default=64, help="distinct pre-generated action rows")
+    p.add_argument("--gather", action="store_true", help="RCCL gather of (obs,reward,done) to rank 0 each step")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    return p.parse_args()
+
+
+def cpu_baseline(args, plants, obstacles):
+    """Oracle (C port of plantos_env.py step/reset) on the host cores: same
+    geometry, same synthetic-action workload, bounded sample (~cpu-seconds)."""
+    sys.path.insert(0, REPO)
+    from oracle import oracle as O
+
+    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    cfg = O.config(args.grid, plants, obstacles, args.range, args.rays)
+    n_envs = min(args.envs, 65536)
+    secs, _ = O.bench(cfg, n_envs, 10, args.seed, threads)  # calibration
+    rate = n_envs * 10 / max(secs, 1e-6)
+    steps = int(max(10, min(2000, args.cpu_seconds * rate / n_envs)))
+    secs, _ = O.bench(cfg, n_envs, steps, args.seed, threads)
+    return {"value": n_envs * steps / secs, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{n_envs} envs x {steps} steps ({secs:.1f} s) of the same synthetic workload, "
+                      f"oracle/plantos_oracle.c, OpenMP {threads} threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(device)
+
+    from plantos_amd import PlantOSBatch
+
+    G, C, R = args.grid, args.rays, args.range
+    plants = args.plants if args.plants is not None else (10 if G <= 32 else 100)
+    obstacles = args.obstacles if args.obstacles is not None else (12 if G <= 32 else 120)
+    n = args.envs
+    b = PlantOSBatch(n, grid_size=G, num_plants=plants, num_obstacles=obstacles, lidar_range=R,
+                     lidar_channels=C, seed=args.seed, env_id_offset=rank * n, device=device)
+    T = args.action_steps
+    actions = torch.empty((T, n), dtype=torch.int32, device=device)
+    for t in range(T):
+        b.synth_actions(args.seed, t, out=actions[t])
+    gather_bufs = None
+    if args.gather and world > 1:
+        gather_bufs = [torch.empty_like(b.obs) for _ in range(world)] if rank == 0 else None
+
+    def one_step(t):
+        b.step(actions[t % T])
+        if args.gather and world > 1:
+            dist.gather(b.obs, gather_bufs, dst=0)
+
+    for t in range(args.warmup):
+        one_step(t)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    K = args.steps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    t0 = time.perf_counter()
+    for k in range(K):
+        ev[k][0].record()
+        one_step(args.warmup + k)
+        ev[k][1].record()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(s.elapsed_time(e) for s, e in ev) / K  # per-launch device time (HIP events)
+    if dist:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    b.raise_on_errors()
+    total_steps = n * K * world
+    value = total_steps / elapsed
+    B = algorithmic_bytes(C, R)
+    achieved = B * n / (kern_ms * 1e-3) / 1e9  # GB/s of ONE launch (one GPU's shard)
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32/f32",
+            "data": "synthetic (device-rng maps, philox actions)",
+            "config": {"workload": f"{n} envs/GPU, {G}x{G} grid, {C} rays, range {R}, {plants} plants, "
+                                   f"{obstacles} obstacles, auto-reset, actions in HBM",
+                       "envs_per_gpu": n, "grid": G, "rays": C, "lidar_range": R,
+                       "parallelism": f"env-shard x{world}" + (" + rccl gather" if args.gather else ""),
+                       "kernel": b.kernel_name},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                         "bytes_per_env_step": B, "kernel_ms": kern_ms},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args, plants, obstacles)
+        print(json.dumps(out), flush=True)
+    b.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

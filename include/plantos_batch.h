@@ -1,0 +1,162 @@
+/*
+ * plantos_batch.h -- C-ABI of the MI355X-native batched PlantOSEnv step/reset.
+ *
+ * Drop-in boundary.  The reference has no native FFI: its
+ * boundary is two Python protocols, and every entry point below replaces one of
+ * them for a whole batch of N envs resident in HBM:
+ *
+ *   pe_create       PlantOSEnv.__init__              plantos_env.py:25-123
+ *                   + DummyVecEnv(env_fns)           A2C_training.py:216-218
+ *   pe_reset        PlantOSEnv.reset                 plantos_env.py:125-158
+ *                   (map generation _generate_map    plantos_env.py:338-372)
+ *   pe_step         PlantOSEnv.step                  plantos_env.py:160-183
+ *                   + DummyVecEnv.step_wait auto-reset (SB3)
+ *   pe_get_info     PlantOSEnv._get_info             plantos_env.py:317-336
+ *   pe_get_state /  the state tuple MCTS clones      mcts_custom_trainer.py:236-241
+ *   pe_set_state    (+ CurriculumWrapper visit_counts injection, A2C_training.py:88-93)
+ *   pe_load_maps    reset() with a host-supplied layout (seed-exact CPython stream mode)
+ *   pe_seed         VecEnv.seed / reset(seed=...)    (the reference ignores it for maps)
+ *   pe_destroy      PlantOSEnv.close                 plantos_env.py:522-528
+ *
+ * Conventions
+ *  - Every array argument is a DEVICE pointer (caller-owned, e.g. a torch tensor on
+ *    the handle's device), row-major, env index outermost.  Only the handle's state
+ *    is owned by the library.
+ *  - Calls are asynchronous on `stream` (a hipStream_t passed as void*; NULL = the
+ *    default stream).  They return PE_OK or a negative PE_ERR_* code; the message of
+ *    the last failure on the calling thread is pe_last_error().
+ *  - A handle is bound to one device and is not re-entrant.
+ *  - No CPU fallback: if the HIP runtime or a gfx950 device is unavailable, pe_create
+ *    fails with PE_ERR_DEVICE.
+ */
+#ifndef PLANTOS_BATCH_H
+#define PLANTOS_BATCH_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PE_ABI_VERSION 1
+
+enum pe_status {
+    PE_OK = 0,
+    PE_ERR_ARG = -1,      /* bad argument / config (Python: ValueError)            */
+    PE_ERR_DEVICE = -2,   /* HIP runtime / device failure                          */
+    PE_ERR_NOMEM = -3,    /* device allocation failed                              */
+    PE_ERR_NOROOM = -4,   /* map generation had no room (plantos_env.py:360-364)  */
+};
+
+/* Per-env scalar slots of the canonical state (pe_get_state / pe_set_state), int32. */
+enum pe_scalar {
+    PE_S_X = 0,        /* rover_pos[0] (row)          plantos_env.py:96  */
+    PE_S_Y = 1,        /* rover_pos[1] (column)                           */
+    PE_S_STEP = 2,     /* step_count                  plantos_env.py:119 */
+    PE_S_COLL = 3,     /* total_collisions            plantos_env.py:123 */
+    PE_S_COLLIDED = 4, /* collided_with_wall          plantos_env.py:121 */
+    PE_S_BONUS = 5,    /* completion_bonus_given      plantos_env.py:122 */
+    PE_S_POISONED = 6, /* bit0: root env would raise TypeError (watering a hydrated
+                          plant, plantos_env.py:217-220); bit1: action < -4 (IndexError);
+                          bit2: last reset had no room (ValueError)                */
+    PE_S_EPISODE = 7,  /* number of resets so far (device-rng stream index)        */
+    PE_NSCAL = 8
+};
+
+/* pe_get_info columns, int32 (plantos_env.py:317-336). */
+enum pe_info {
+    PE_I_X = 0, PE_I_Y, PE_I_THIRSTY, PE_I_HYDRATED, PE_I_TOTAL_PLANTS, PE_I_STEP,
+    PE_I_EXPLORED, PE_I_TOTAL_CELLS, PE_I_COLLIDED, PE_I_COLLISIONS, PE_I_POISONED,
+    PE_NINFO
+};
+
+/* Cell codes of the canonical grid (obstacles set + plants dict, plantos_env.py:97-98). */
+enum pe_cell { PE_EMPTY = 0, PE_OBSTACLE = 1, PE_HYDRATED = 2, PE_THIRSTY = 3 };
+
+typedef struct pe_config {
+    int32_t abi_version;        /* = PE_ABI_VERSION */
+    int32_t grid_size;          /* G, plantos_env.py:25 (device: 1..128)        */
+    int32_t num_plants;         /* P                                            */
+    int32_t num_obstacles;      /* O -> O/3 clusters, plantos_env.py:341        */
+    int32_t lidar_range;        /* R (device: 1..64)                            */
+    int32_t lidar_channels;     /* C (device: 1..256)                           */
+    int32_t max_steps;          /* 1000, plantos_env.py:120                     */
+    int32_t autoreset;          /* 1: pe_step resets done envs (DummyVecEnv)    */
+    double thirsty_plant_prob;  /* 0.7, plantos_env.py:26                       */
+    double r_goal, r_mistake, r_invalid, r_water_empty; /* plantos_env.py:76-79 */
+    double r_step, r_exploration, r_revisit, r_complete; /* plantos_env.py:80-83 */
+    uint64_t seed;              /* device-rng key (Philox4x32-10)               */
+    uint32_t env_id_offset;     /* global id of env 0 (sharding across GPUs)    */
+    int32_t reserved[7];
+} pe_config;
+
+typedef struct pe_handle pe_handle;
+
+/* Fill `c` with the reference defaults for the given geometry
+ * (plantos_env.py:25-27, 76-83, 120). */
+void pe_default_config(pe_config* c, int32_t grid_size, int32_t num_plants, int32_t num_obstacles,
+                       int32_t lidar_range, int32_t lidar_channels);
+
+/* Observation length 5*C + 2 + 25 (plantos_env.py:55-57). */
+int32_t pe_obs_dim(const pe_config* c);
+
+/* Allocate the SoA state for n_envs envs on `device`. All envs start reset (episode 0). */
+int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** out);
+int pe_destroy(pe_handle* h);
+
+/* Re-key the device RNG (and optionally zero the episode counters). */
+int pe_seed(pe_handle* h, uint64_t seed, int32_t reset_episode_counters);
+
+/* Reset the envs whose mask byte is non-zero (all envs when mask == NULL) with the
+ * device-rng map generator, then write obs[n_envs, D] for ALL envs (reset ones get
+ * their fresh obs, the others their current obs). */
+int pe_reset(pe_handle* h, const uint8_t* mask_or_null, float* obs, void* stream);
+
+/* One step of every env.
+ *   actions      int32[n] or int64[n] (action_bytes = 4 or 8); 0..3 move N/E/S/W, >=4 water
+ *   obs          f32[n, D]   post-step obs (post-reset obs for done envs when autoreset)
+ *   reward       f32[n]      reward (computed in f64 like the reference, cast once)
+ *   terminated   u8[n], truncated u8[n]
+ *   terminal_obs f32[n, D] or NULL: rows of done envs receive the pre-reset obs
+ *   episode_return f64[n] or NULL: rows of done envs receive the episode's f64 return
+ *   episode_length i32[n] or NULL: rows of done envs receive the episode length      */
+int pe_step(pe_handle* h, const void* actions, int32_t action_bytes, float* obs, float* reward,
+            uint8_t* terminated, uint8_t* truncated, float* terminal_obs_or_null,
+            double* episode_return_or_null, int32_t* episode_length_or_null, void* stream);
+
+/* info columns (pe_info) for all envs: int32[n, PE_NINFO]. */
+int pe_get_info(pe_handle* h, int32_t* info, void* stream);
+
+/* Canonical state, reference terms: cells u8[n,G,G] (pe_cell), visits i32[n,G,G],
+ * explored i8[n,G,G] (0/1/2), scalars i32[n,PE_NSCAL].  Any pointer may be NULL
+ * (get: skipped; set: that part is left unchanged).  set recomputes derived
+ * counters (explored/total cells) from the arrays. Visits saturate at 65535. */
+int pe_get_state(pe_handle* h, uint8_t* cells, int32_t* visits, int8_t* explored, int32_t* scalars,
+                 void* stream);
+int pe_set_state(pe_handle* h, const uint8_t* cells, const int32_t* visits, const int8_t* explored,
+                 const int32_t* scalars, void* stream);
+
+/* Reset k envs (env_index i32[k]) to host-supplied layouts: cells u8[k,G,G] (obstacles
+ * and plants only), rover i32[k,2]; then write obs[k, D] for those envs (row j = env
+ * env_index[j]).  Used by the seed-exact CPython-stream reset mode. */
+int pe_load_maps(pe_handle* h, int32_t k, const int32_t* env_index, const uint8_t* cells,
+                 const int32_t* rover, float* obs_k, void* stream);
+
+/* Synthetic benchmark actions: actions[e] = philox(seed, env_id_offset+e, t) % 5. */
+int pe_synth_actions(pe_handle* h, uint64_t seed, uint32_t t, int32_t* actions, void* stream);
+
+/* Accumulated error bits OR-ed over all envs since the last call (PE_S_POISONED bit
+ * layout); synchronizes the stream. */
+int pe_poll_errors(pe_handle* h, int32_t* bits, void* stream);
+
+/* Introspection for tests / benchmarks. */
+int32_t pe_num_envs(const pe_handle* h);
+int32_t pe_kernel_variant(const pe_handle* h);  /* 0 generic, >0 specialized geometry */
+const char* pe_kernel_name(const pe_handle* h);
+uint64_t pe_state_bytes(const pe_handle* h);
+
+const char* pe_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

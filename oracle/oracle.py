@@ -133,11 +133,11 @@ class Batch:
                             _p(self.scal), _p(a), _p(obs), _p(rew), _p(te), _p(tr))
         return obs, rew, te.astype(bool), tr.astype(bool)
 
-    def obs(self):
+    def obs(self, idx=None):
         self._chk()
         D = obs_dim(self.cfg)
         out = np.zeros((self.n, D), np.float32)
-        for e in range(self.n):
+        for e in (range(self.n) if idx is None else idx):
             lib().po_obs(ctypes.byref(self.cfg), _p(self.cells[e]), _p(self.visits[e]), _p(self.scal[e]),
                          _p(out[e]))
         return out

@@ -1,0 +1,309 @@
+// pe_device.hpp -- device-side state layout and per-env primitives of the
+// batched PlantOSEnv (MI355X / gfx950).
+//
+// HBM layout (struct-of-arrays, env-major records):
+//   scal   uint4  [N]              packed scalars (below), one 16-B load per lane
+//   ep_ret f64    [N]              running episode return (Monitor semantics)
+//   grid   u64    [N][G][WPR]      2-bit cell codes, each row padded by R obstacle
+//                                  cells on both sides: a LIDAR probe never needs a
+//                                  column bounds test (off-map == obstacle,
+//                                  plantos_env.py:271-274)
+//   vis    u32    [N][G][NW]       4-bit saturating visit counts min(v,15), padded by
+//                                  2 cells of value 10 on both sides (off-map reads
+//                                  1.0 = min(10,10)/10, plantos_env.py:307-311)
+//   v16    u16    [N][G*G]         exact visit counts (saturating at 65535), touched
+//                                  once per successful move (plantos_env.py:203)
+//   expl   u32    [N][EW]          explored bitmap (explored_map > 0)
+//
+// Packed scalars (scal):
+//   w0 = x | y<<8 | step<<16        w1 = explored_count | total_cells<<16
+//   w2 = collisions | flags<<16     w3 = episode (resets so far)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pe {
+
+enum : int { EMPTY = 0, OBST = 1, HYD = 2, THIRSTY = 3 };
+
+// flags (high half of w2)
+enum : uint32_t {
+  F_COLLIDED = 1u,      // collided_with_wall (sticky)
+  F_BONUS = 2u,         // completion_bonus_given
+  F_POISON_HYD = 4u,    // root env would raise TypeError (plantos_env.py:217-220)
+  F_POISON_ACT = 8u,    // action < -4 (reference IndexError)
+  F_NOROOM = 16u,       // last reset had no room (plantos_env.py:360-364)
+};
+
+constexpr uint64_t kEven64 = 0x5555555555555555ull;  // low bit of every 2-bit code
+constexpr uint32_t kDomainReset = 0x50455352u;        // Philox counter domain words
+constexpr uint32_t kDomainAction = 0x4E544341u;       // (must match oracle/plantos_oracle.c)
+constexpr int kMaxWPR = 8;                            // G + 2R <= 256
+constexpr int kMaxNW = 20;                            // (G + 4) * 4 bits + 1 word
+
+struct Geo {
+  int G, C, R, D, DS;   // D = 5C+27 obs floats, DS = LDS row stride (odd)
+  int WPR, NW, EW, GG;
+  int64_t gstride, vstride, hstride, estride;  // per-env strides in elements
+};
+
+// Host-built constant tables (one copy per handle, global memory, read-only).
+struct Tables {
+  float dist[72];              // dist[r] = float(r / R)             plantos_env.py:288
+  float pos[256];              // pos[x]  = float(x / G)             plantos_env.py:295-296
+  float vis[16];               // vis[n]  = float(min(n,10) / 10.0)  plantos_env.py:308
+  uint64_t grid_pad[kMaxWPR];  // empty row: obstacle codes in the 2R pad columns
+  uint64_t grid_real[kMaxWPR]; // low-bit mask of the G real columns
+  uint32_t vis_pad[kMaxNW];    // empty visit row: nibble 10 in the 4 pad columns
+};
+
+struct State {
+  uint4* scal;
+  double* ep_ret;
+  uint64_t* grid;
+  uint32_t* vis;
+  uint16_t* v16;
+  uint32_t* expl;
+  const Tables* tab;
+  const signed char* ldx;  // [C][R] LIDAR offsets (generic kernel)
+  const signed char* ldy;
+  uint32_t* err_bits;      // OR of error flags raised since the last poll
+};
+
+struct Rules {
+  double r_goal, r_mistake, r_invalid, r_water_empty, r_step, r_exploration, r_revisit, r_complete;
+  double p_thirsty;
+  uint64_t seed;
+  uint32_t env_off;
+  int P, O, max_steps;
+};
+
+// ------------------------------------------------------------------ scalars
+struct Scal {
+  int x, y, step, expl, total, coll;
+  uint32_t flags, episode;
+};
+
+__device__ __forceinline__ Scal unpack(uint4 w) {
+  Scal s;
+  s.x = w.x & 0xFF;
+  s.y = (w.x >> 8) & 0xFF;
+  s.step = w.x >> 16;
+  s.expl = w.y & 0xFFFF;
+  s.total = w.y >> 16;
+  s.coll = w.z & 0xFFFF;
+  s.flags = w.z >> 16;
+  s.episode = w.w;
+  return s;
+}
+
+__device__ __forceinline__ uint4 pack(const Scal& s) {
+  uint4 w;
+  w.x = (uint32_t)s.x | ((uint32_t)s.y << 8) | ((uint32_t)s.step << 16);
+  w.y = (uint32_t)s.expl | ((uint32_t)s.total << 16);
+  w.z = (uint32_t)s.coll | (s.flags << 16);
+  w.w = s.episode;
+  return w;
+}
+
+// ------------------------------------------------------------------ Philox4x32-10
+__device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+    uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// Sequential u32 stream over Philox blocks: identical draw order to the oracle's
+// u32src (oracle/plantos_oracle.c) for (seed, env_id, episode).
+struct Stream {
+  uint32_t k0, k1, env, episode, blk;
+  uint32_t buf[4];
+  int pos;
+  __device__ void init(uint64_t seed, uint32_t env_id, uint32_t ep) {
+    k0 = (uint32_t)seed;
+    k1 = (uint32_t)(seed >> 32);
+    env = env_id;
+    episode = ep;
+    blk = 0;
+    pos = 4;
+  }
+  __device__ uint32_t next() {
+    if (pos == 4) {
+      uint4 o = philox(make_uint4(blk, env, episode, kDomainReset), k0, k1);
+      buf[0] = o.x; buf[1] = o.y; buf[2] = o.z; buf[3] = o.w;
+      ++blk;
+      pos = 0;
+    }
+    uint32_t v = buf[0];
+    // select without dynamic register indexing
+    v = pos == 1 ? buf[1] : v;
+    v = pos == 2 ? buf[2] : v;
+    v = pos == 3 ? buf[3] : v;
+    ++pos;
+    return v;
+  }
+  // random.py:239-248 _randbelow_with_getrandbits (getrandbits(k) = u32 >> (32-k))
+  __device__ uint32_t below(uint32_t n) {
+    if (!n) return 0;
+    int k = 32 - __clz(n);
+    uint32_t r = next() >> (32 - k);
+    while (r >= n) r = next() >> (32 - k);
+    return r;
+  }
+  // random.random()
+  __device__ double random53() {
+    uint32_t a = next() >> 5, b = next() >> 6;
+    return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
+  }
+};
+
+// ------------------------------------------------------------------ cell access
+__device__ __forceinline__ int grid_code(const State& st, const Geo& g, int64_t e, int row, int pcol) {
+  int bit = 2 * pcol;
+  uint64_t w = st.grid[e * g.gstride + (int64_t)row * g.WPR + (bit >> 6)];
+  return (int)((w >> (bit & 63)) & 3u);
+}
+
+__device__ __forceinline__ void grid_set(const State& st, const Geo& g, int64_t e, int row, int pcol, int code) {
+  int bit = 2 * pcol;
+  uint64_t* p = st.grid + e * g.gstride + (int64_t)row * g.WPR + (bit >> 6);
+  uint64_t w = *p;
+  w &= ~(3ull << (bit & 63));
+  w |= (uint64_t)code << (bit & 63);
+  *p = w;
+}
+
+// 5 nibbles (padded columns y..y+4 == real columns y-2..y+2) of one visit row.
+__device__ __forceinline__ uint32_t vis_window(const State& st, const Geo& g, int64_t e, int row, int y) {
+  int bit = 4 * y;
+  const uint32_t* p = st.vis + e * g.vstride + (int64_t)row * g.NW + (bit >> 5);
+  uint64_t two = (uint64_t)p[0] | ((uint64_t)p[1] << 32);
+  return (uint32_t)(two >> (bit & 31)) & 0xFFFFFu;
+}
+
+__device__ __forceinline__ void vis_set(const State& st, const Geo& g, int64_t e, int row, int col, uint32_t v) {
+  int bit = 4 * (col + 2);
+  uint32_t* p = st.vis + e * g.vstride + (int64_t)row * g.NW + (bit >> 5);
+  uint32_t w = *p;
+  w &= ~(0xFu << (bit & 31));
+  w |= v << (bit & 31);
+  *p = w;
+}
+
+__device__ __forceinline__ bool expl_test_set(const State& st, const Geo& g, int64_t e, int cell) {
+  uint32_t* p = st.expl + e * g.estride + (cell >> 5);
+  uint32_t m = 1u << (cell & 31);
+  uint32_t w = *p;
+  if (w & m) return false;
+  *p = w | m;
+  return true;
+}
+
+// ------------------------------------------------------------------ map generation
+// Index of the j-th real cell (row-major) whose code matches `kind`
+// (kind 0: not an obstacle, kind 1: empty).  Returns the cell id x*G+y.
+__device__ inline int nth_cell(const State& st, const Geo& g, int64_t e, int j, int kind) {
+  for (int row = 0; row < g.G; ++row) {
+    for (int w = 0; w < g.WPR; ++w) {
+      uint64_t v = st.grid[e * g.gstride + (int64_t)row * g.WPR + w];
+      uint64_t lo = v & kEven64, hi = (v >> 1) & kEven64;
+      uint64_t real = st.tab->grid_real[w];
+      uint64_t m = kind == 0 ? (real & ~(lo & ~hi)) : (real & ~(lo | hi));
+      int c = __popcll(m);
+      if (j < c) {
+        for (int k = 0; k < j; ++k) m &= m - 1;
+        int pcol = w * 32 + (__ffsll((unsigned long long)m) - 1) / 2;
+        return row * g.G + (pcol - g.R);
+      }
+      j -= c;
+    }
+  }
+  return 0;  // unreachable when j < count
+}
+
+// reset() for one env (plantos_env.py:125-158, _generate_map 338-372) in the
+// device-rng mode defined by oracle po_reset_philox: Philox stream keyed by
+// (seed, global env id, episode); candidate lists in row-major order.
+// Writes all state of env e; returns the new scalars.
+__device__ inline Scal reset_env(const State& st, const Geo& g, const Rules& rl, int64_t e, uint32_t episode) {
+  const int G = g.G;
+  // clear
+  for (int row = 0; row < G; ++row) {
+    for (int w = 0; w < g.WPR; ++w) st.grid[e * g.gstride + (int64_t)row * g.WPR + w] = st.tab->grid_pad[w];
+    for (int w = 0; w < g.NW; ++w) st.vis[e * g.vstride + (int64_t)row * g.NW + w] = st.tab->vis_pad[w];
+  }
+  uint32_t* v32 = reinterpret_cast<uint32_t*>(st.v16 + e * g.hstride);
+  for (int k = 0; k < (int)(g.hstride / 2); ++k) v32[k] = 0u;
+  for (int k = 0; k < g.estride; ++k) st.expl[e * g.estride + k] = 0u;
+
+  Stream rng;
+  rng.init(rl.seed, rl.env_off + (uint32_t)e, episode);
+  // obstacle clusters, plantos_env.py:341-354
+  const int clusters = rl.O / 3;
+  for (int q = 0; q < clusters; ++q) {
+    int cx = 2 + (int)rng.below((uint32_t)(G - 4));
+    int cy = 2 + (int)rng.below((uint32_t)(G - 4));
+    int size = 2 + (int)rng.below(2u);
+    for (int dx = 0; dx < size; ++dx)
+      for (int dy = 0; dy < size; ++dy) {
+        int ox = cx + dx - size / 2, oy = cy + dy - size / 2;
+        if (0 <= ox && ox < G && 0 <= oy && oy < G) grid_set(st, g, e, ox, oy + g.R, OBST);
+      }
+  }
+  int n_obst = 0;
+  for (int row = 0; row < G; ++row)
+    for (int w = 0; w < g.WPR; ++w) {
+      uint64_t v = st.grid[e * g.gstride + (int64_t)row * g.WPR + w];
+      n_obst += __popcll(v & ~(v >> 1) & st.tab->grid_real[w] & kEven64);
+    }
+  const int nfree = g.GG - n_obst;
+  Scal s;
+  s.step = 0;
+  s.coll = 0;
+  s.flags = 0;
+  s.episode = episode + 1u;
+  s.total = nfree;
+  s.expl = 1;
+  if (nfree < rl.P + 1) {  // ValueError, plantos_env.py:360-364
+    s.flags = F_NOROOM;
+    s.x = 0;
+    s.y = 0;
+    s.expl = 0;
+    atomicOr(st.err_bits, F_NOROOM);
+    return s;
+  }
+  // random.sample(list(available), P): set-based selection, row-major list
+  uint16_t* picks = st.v16 + e * g.hstride;  // scratch: pick order (cleared below)
+  for (int i = 0; i < rl.P; ++i) {
+    int c;
+    for (;;) {
+      int j = (int)rng.below((uint32_t)nfree);
+      c = nth_cell(st, g, e, j, 0);
+      if (grid_code(st, g, e, c / G, c % G + g.R) == EMPTY) break;  // else already selected
+    }
+    grid_set(st, g, e, c / G, c % G + g.R, HYD);
+    picks[i] = (uint16_t)c;
+  }
+  // thirsty draws in sample order, plantos_env.py:367-369
+  for (int i = 0; i < rl.P; ++i) {
+    int c = picks[i];
+    if (rng.random53() < rl.p_thirsty) grid_set(st, g, e, c / G, c % G + g.R, THIRSTY);
+  }
+  for (int i = 0; i < rl.P; ++i) picks[i] = 0;
+  // rover: choice(list(available - plants)), plantos_env.py:370-372
+  int rc = nth_cell(st, g, e, (int)rng.below((uint32_t)(nfree - rl.P)), 1);
+  s.x = rc / G;
+  s.y = rc % G;
+  st.v16[e * g.hstride + rc] = 1;  // plantos_env.py:146-147
+  vis_set(st, g, e, s.x, s.y, 1u);
+  expl_test_set(st, g, e, rc);     // plantos_env.py:236
+  return s;
+}
+
+}  // namespace pe

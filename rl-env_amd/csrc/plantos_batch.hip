@@ -1,0 +1,929 @@
+// plantos_batch.hip -- MI355X (gfx950) batched PlantOSEnv step/reset + C-ABI.
+//
+// One lane owns one env (no cross-env writes, so no atomics on state).  The fused
+// step kernel does, per env: action decode, move/collide or water, visit/explored
+// update, f64 reward (cast once), terminated/truncated, optional auto-reset, LIDAR
+// ray-march, position, 5x5 visit slice; each lane assembles its obs row in LDS and
+// the workgroup streams the contiguous [BLOCK x D] obs tile to HBM with 16-byte
+// stores.  C-ABI: include/plantos_batch.h.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "../../include/plantos_batch.h"
+#include "lidar_tables.inc"
+#include "pe_device.hpp"
+
+using namespace pe;
+
+namespace {
+
+constexpr int kBlock = 64;      // envs per workgroup (one wave)
+constexpr int kTabFloats = 344; // Tables::dist + pos + vis
+
+struct StepArgs {
+  State st;
+  Geo g;
+  Rules rl;
+  int n;
+  int autoreset;
+  int act_bytes;
+  const void* actions;
+  float* obs;
+  float* reward;
+  uint8_t* term;
+  uint8_t* trunc;
+  float* tobs;
+  double* ep_ret_out;
+  int32_t* ep_len_out;
+  const uint8_t* mask;  // reset kernel
+};
+
+// ------------------------------------------------------------------ obs builders
+// _get_lidar_obs, plantos_env.py:251-315, into one LDS row.
+
+// Generic: runtime (G, C, R), LIDAR offsets from the handle's table.
+__device__ __forceinline__ void build_obs_generic(const StepArgs& a, int64_t e, int x, int y, float* row,
+                                                  const float* tdist, const float* tpos, const float* tvis) {
+  const Geo& g = a.g;
+  const int R = g.R, C = g.C;
+  for (int i = 0; i < C; ++i) {
+    int dist = R, ent = EMPTY;
+    for (int r = 1; r <= R; ++r) {
+      int cx = x + a.st.ldx[i * R + r - 1];
+      int cy = y + a.st.ldy[i * R + r - 1];
+      int code = (cx >= 0 && cx < g.G) ? grid_code(a.st, g, e, cx, cy + R) : OBST;  // :271-284
+      if (code != EMPTY) {
+        dist = r;
+        ent = code;
+        break;
+      }
+    }
+    row[5 * i] = tdist[dist];
+    row[5 * i + 1] = ent == 0 ? 1.0f : 0.0f;
+    row[5 * i + 2] = ent == 1 ? 1.0f : 0.0f;
+    row[5 * i + 3] = ent == 2 ? 1.0f : 0.0f;
+    row[5 * i + 4] = ent == 3 ? 1.0f : 0.0f;
+  }
+  row[5 * C] = tpos[x];
+  row[5 * C + 1] = tpos[y];
+  for (int lx = 0; lx < 5; ++lx) {
+    int xr = x + lx - 2;
+    uint32_t win = (xr >= 0 && xr < g.G) ? vis_window(a.st, g, e, xr, y) : 0xAAAAAu;
+    for (int ly = 0; ly < 5; ++ly) row[5 * C + 2 + 5 * lx + ly] = tvis[(win >> (4 * ly)) & 15u];
+  }
+}
+
+// Specialized: compile-time (C, R) offsets; the (2R+1) window rows around the rover
+// are loaded once and every probe is a constant-shift 2-bit extract.
+template <int C, int R, bool ONEWORD>
+__device__ __forceinline__ void build_obs_static(const StepArgs& a, int64_t e, int x, int y, float* row,
+                                                 const float* tpos, const float* tvis) {
+  constexpr int W = 2 * R + 1;
+  static_assert(2 * W <= 64, "window must fit one u64");
+  const Geo& g = a.g;
+  const uint64_t* gbase = a.st.grid + e * g.gstride;
+  uint64_t win[W];
+  const int bit = 2 * y;
+#pragma unroll
+  for (int k = 0; k < W; ++k) {
+    int xr = x + k - R;
+    uint64_t v = kEven64;  // off-map row: every cell reads as obstacle
+    if (xr >= 0 && xr < g.G) {
+      if constexpr (ONEWORD) {
+        v = gbase[xr] >> bit;
+      } else {
+        const uint64_t* p = gbase + (int64_t)xr * g.WPR + (bit >> 6);
+        int o = bit & 63;
+        uint64_t lo = p[0];
+        uint64_t hi = ((bit >> 6) + 1 < g.WPR) ? p[1] : 0ull;
+        v = o ? ((lo >> o) | (hi << (64 - o))) : lo;
+      }
+    }
+    win[k] = v;
+  }
+  using T = LidarTab<C, R>;
+#pragma unroll
+  for (int i = 0; i < C; ++i) {
+    float dist = 1.0f;  // R/R
+    int ent = EMPTY;
+#pragma unroll
+    for (int r = R; r >= 1; --r) {
+      const int dx = T::dx[i][r - 1], dy = T::dy[i][r - 1];
+      int code = (int)((win[dx + R] >> (2 * (dy + R))) & 3u);
+      if (code != EMPTY) {
+        dist = (float)((double)r / (double)R);  // constant-folded: float(r/R), :288
+        ent = code;
+      }
+    }
+    row[5 * i] = dist;
+    row[5 * i + 1] = ent == 0 ? 1.0f : 0.0f;
+    row[5 * i + 2] = ent == 1 ? 1.0f : 0.0f;
+    row[5 * i + 3] = ent == 2 ? 1.0f : 0.0f;
+    row[5 * i + 4] = ent == 3 ? 1.0f : 0.0f;
+  }
+  row[5 * C] = tpos[x];
+  row[5 * C + 1] = tpos[y];
+#pragma unroll
+  for (int lx = 0; lx < 5; ++lx) {
+    int xr = x + lx - 2;
+    uint32_t w5 = (xr >= 0 && xr < g.G) ? vis_window(a.st, g, e, xr, y) : 0xAAAAAu;
+#pragma unroll
+    for (int ly = 0; ly < 5; ++ly) row[5 * C + 2 + 5 * lx + ly] = tvis[(w5 >> (4 * ly)) & 15u];
+  }
+}
+
+template <int VC, int VR, bool ONEWORD>
+__device__ __forceinline__ void build_obs(const StepArgs& a, int64_t e, int x, int y, float* row, const float* tdist,
+                                          const float* tpos, const float* tvis) {
+  if constexpr (VC == 0) {
+    build_obs_generic(a, e, x, y, row, tdist, tpos, tvis);
+  } else {
+    build_obs_static<VC, VR, ONEWORD>(a, e, x, y, row, tpos, tvis);
+  }
+}
+
+// ------------------------------------------------------------------ transition
+// PlantOSEnv.step without the observation (plantos_env.py:160-183, 185-222).
+__device__ __forceinline__ double transition(const StepArgs& a, int64_t e, Scal& s, int64_t action, bool& term,
+                                             bool& trunc) {
+  const Geo& g = a.g;
+  const Rules& rl = a.rl;
+  s.step = s.step < 65535 ? s.step + 1 : 65535;  // :162
+  double h = 0.0;
+  if (action < 4) {                                // :166
+    int64_t ai = action < 0 ? action + 4 : action; // Python negative list index
+    if (ai < 0) {
+      s.flags |= F_POISON_ACT;                     // reference: IndexError
+      atomicOr(a.st.err_bits, F_POISON_ACT);
+    } else {
+      // directions (:186) N,E,S,W = (-1,0),(0,1),(1,0),(0,-1)
+      const int dxm = ai == 0 ? -1 : (ai == 2 ? 1 : 0);
+      const int dym = ai == 1 ? 1 : (ai == 3 ? -1 : 0);
+      const int nx = s.x + dxm, ny = s.y + dym;
+      bool ok = nx >= 0 && nx < g.G && ny >= 0 && ny < g.G;  // :193-195
+      if (ok) ok = grid_code(a.st, g, e, nx, ny + g.R) != OBST;
+      if (ok) {
+        const int cell = nx * g.G + ny;
+        uint16_t* vp = a.st.v16 + e * g.hstride + cell;
+        const uint32_t v = *vp;
+        const bool never = v == 0;                              // :197
+        const uint32_t v1 = v < 65535u ? v + 1u : 65535u;       // :203
+        *vp = (uint16_t)v1;
+        vis_set(a.st, g, e, nx, ny, v1 < 15u ? v1 : 15u);
+        if (expl_test_set(a.st, g, e, s.x * g.G + s.y)) s.expl++;  // explored[old] = 1, :198
+        if (expl_test_set(a.st, g, e, cell)) s.expl++;             // explored[new] = 2, :200
+        s.x = nx;                                                  // :199
+        s.y = ny;
+        h = never ? rl.r_exploration : rl.r_revisit;               // :204-207
+      } else {
+        s.flags |= F_COLLIDED;                                     // :209
+        s.coll = s.coll < 65535 ? s.coll + 1 : 65535;              // :210
+        h = rl.r_invalid;                                          // :211
+      }
+    }
+  } else {
+    const int code = grid_code(a.st, g, e, s.x, s.y + g.R);
+    if (code == THIRSTY) {                                         // fork plantos_env_new.py:237-240
+      grid_set(a.st, g, e, s.x, s.y + g.R, HYD);
+      h = rl.r_goal;
+    } else if (code == HYD) {                                      // fork :241-242 (root raises)
+      h = rl.r_mistake;
+      if (!(s.flags & F_POISON_HYD)) atomicOr(a.st.err_bits, F_POISON_HYD);
+      s.flags |= F_POISON_HYD;
+    } else {
+      h = rl.r_water_empty;                                        // :221-222
+    }
+  }
+  double rew = rl.r_step;                                          // :164
+  rew += h;
+  // exploration_percentage >= 100  <=>  explored >= total  (:176, 244-246, 331)
+  term = s.expl >= s.total;
+  trunc = s.step >= rl.max_steps;                                  // :177
+  if (term && !(s.flags & F_BONUS)) {                              // :179-181
+    rew += rl.r_complete;
+    s.flags |= F_BONUS;
+  }
+  return rew;
+}
+
+__device__ __forceinline__ void load_tables(float* smem, const Tables* tab) {
+  const float* src = reinterpret_cast<const float*>(tab);
+  for (int k = threadIdx.x; k < kTabFloats; k += blockDim.x) smem[k] = src[k];
+}
+
+// Stream the block's [valid x D] obs tile (LDS rows of stride DS) to HBM.
+__device__ __forceinline__ void store_tile(const float* rows, float* dst, int valid, int D, int DS) {
+  const int total = valid * D;
+  if (DS == D) {
+    if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+      const int n4 = total >> 2;
+      const float4* s4 = reinterpret_cast<const float4*>(rows);
+      float4* d4 = reinterpret_cast<float4*>(dst);
+      for (int k = threadIdx.x; k < n4; k += blockDim.x) d4[k] = s4[k];
+      for (int k = (n4 << 2) + threadIdx.x; k < total; k += blockDim.x) dst[k] = rows[k];
+    } else {
+      for (int k = threadIdx.x; k < total; k += blockDim.x) dst[k] = rows[k];
+    }
+  } else {
+    for (int k = threadIdx.x; k < total; k += blockDim.x) {
+      int r = k / D, c = k - r * D;
+      dst[k] = rows[r * DS + c];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ kernels
+template <int VC, int VR, bool ONEWORD>
+__global__ __launch_bounds__(kBlock) void pe_step_kernel(StepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* tdist = smem;
+  float* tpos = smem + 72;
+  float* tvis = smem + 328;
+  float* rows = smem + kTabFloats;
+  load_tables(smem, a.st.tab);
+  __syncthreads();
+  const int64_t e0 = (int64_t)blockIdx.x * kBlock;
+  const int64_t e = e0 + threadIdx.x;
+  float* row = rows + threadIdx.x * a.g.DS;
+  if (e < a.n) {
+    int64_t action = a.act_bytes == 8 ? reinterpret_cast<const int64_t*>(a.actions)[e]
+                                       : (int64_t)reinterpret_cast<const int32_t*>(a.actions)[e];
+    Scal s = unpack(a.st.scal[e]);
+    bool term = false, trunc = false;
+    double rew = transition(a, e, s, action, term, trunc);
+    double ret = a.st.ep_ret[e] + rew;
+    a.reward[e] = (float)rew;
+    a.term[e] = term;
+    a.trunc[e] = trunc;
+    if ((term || trunc) && a.autoreset) {
+      // DummyVecEnv.step_wait: keep the terminal obs, reset, return the reset obs.
+      if (a.tobs) {
+        build_obs<VC, VR, ONEWORD>(a, e, s.x, s.y, row, tdist, tpos, tvis);
+        float* t = a.tobs + e * a.g.D;
+        for (int k = 0; k < a.g.D; ++k) t[k] = row[k];
+      }
+      if (a.ep_ret_out) a.ep_ret_out[e] = ret;
+      if (a.ep_len_out) a.ep_len_out[e] = s.step;
+      s = reset_env(a.st, a.g, a.rl, e, s.episode);
+      ret = 0.0;
+    }
+    a.st.ep_ret[e] = ret;
+    a.st.scal[e] = pack(s);
+    build_obs<VC, VR, ONEWORD>(a, e, s.x, s.y, row, tdist, tpos, tvis);
+  }
+  __syncthreads();
+  const int64_t valid = a.n - e0 < kBlock ? a.n - e0 : kBlock;
+  store_tile(rows, a.obs + e0 * a.g.D, (int)valid, a.g.D, a.g.DS);
+}
+
+// reset(): masked device-rng reset, then obs of every env (obs may be NULL).
+template <int VC, int VR, bool ONEWORD>
+__global__ __launch_bounds__(kBlock) void pe_reset_kernel(StepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* tdist = smem;
+  float* tpos = smem + 72;
+  float* tvis = smem + 328;
+  float* rows = smem + kTabFloats;
+  load_tables(smem, a.st.tab);
+  __syncthreads();
+  const int64_t e0 = (int64_t)blockIdx.x * kBlock;
+  const int64_t e = e0 + threadIdx.x;
+  float* row = rows + threadIdx.x * a.g.DS;
+  if (e < a.n) {
+    Scal s = unpack(a.st.scal[e]);
+    if (!a.mask || a.mask[e]) {
+      s = reset_env(a.st, a.g, a.rl, e, s.episode);
+      a.st.ep_ret[e] = 0.0;
+      a.st.scal[e] = pack(s);
+    }
+    if (a.obs) build_obs<VC, VR, ONEWORD>(a, e, s.x, s.y, row, tdist, tpos, tvis);
+  }
+  if (!a.obs) return;
+  __syncthreads();
+  const int64_t valid = a.n - e0 < kBlock ? a.n - e0 : kBlock;
+  store_tile(rows, a.obs + e0 * a.g.D, (int)valid, a.g.D, a.g.DS);
+}
+
+// pe_load_maps: host-supplied layouts (CPython-stream reset mode).
+__global__ __launch_bounds__(kBlock) void pe_load_maps_kernel(StepArgs a, int k, const int32_t* idx,
+                                                              const uint8_t* cells, const int32_t* rover) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* tdist = smem;
+  float* tpos = smem + 72;
+  float* tvis = smem + 328;
+  float* rows = smem + kTabFloats;
+  load_tables(smem, a.st.tab);
+  __syncthreads();
+  const int j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= k) return;
+  const Geo& g = a.g;
+  const int64_t e = idx[j];
+  const uint8_t* c = cells + (int64_t)j * g.GG;
+  int n_obst = 0;
+  for (int row = 0; row < g.G; ++row) {
+    for (int w = 0; w < g.WPR; ++w) a.st.grid[e * g.gstride + (int64_t)row * g.WPR + w] = a.st.tab->grid_pad[w];
+    for (int w = 0; w < g.NW; ++w) a.st.vis[e * g.vstride + (int64_t)row * g.NW + w] = a.st.tab->vis_pad[w];
+    for (int col = 0; col < g.G; ++col) {
+      int code = c[row * g.G + col] & 3;
+      n_obst += code == OBST;
+      if (code) grid_set(a.st, g, e, row, col + g.R, code);
+    }
+  }
+  uint32_t* v32 = reinterpret_cast<uint32_t*>(a.st.v16 + e * g.hstride);
+  for (int q = 0; q < (int)(g.hstride / 2); ++q) v32[q] = 0u;
+  for (int q = 0; q < g.estride; ++q) a.st.expl[e * g.estride + q] = 0u;
+  Scal s = unpack(a.st.scal[e]);
+  s.x = rover[2 * j];
+  s.y = rover[2 * j + 1];
+  s.step = 0;
+  s.coll = 0;
+  s.flags = 0;
+  s.episode += 1u;
+  s.total = g.GG - n_obst;
+  s.expl = 1;
+  const int rc = s.x * g.G + s.y;
+  a.st.v16[e * g.hstride + rc] = 1;
+  vis_set(a.st, g, e, s.x, s.y, 1u);
+  expl_test_set(a.st, g, e, rc);
+  a.st.scal[e] = pack(s);
+  a.st.ep_ret[e] = 0.0;
+  float* row = rows + threadIdx.x * g.DS;
+  build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis);
+  if (a.obs)
+    for (int q = 0; q < g.D; ++q) a.obs[(int64_t)j * g.D + q] = row[q];
+}
+
+// _get_info (plantos_env.py:317-336), integer columns.
+__global__ void pe_info_kernel(StepArgs a, int32_t* info) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.n) return;
+  const Geo& g = a.g;
+  Scal s = unpack(a.st.scal[e]);
+  int th = 0, hy = 0;
+  for (int row = 0; row < g.G; ++row)
+    for (int w = 0; w < g.WPR; ++w) {
+      uint64_t v = a.st.grid[e * g.gstride + (int64_t)row * g.WPR + w];
+      uint64_t lo = v & kEven64, hi = (v >> 1) & kEven64, real = a.st.tab->grid_real[w];
+      th += __popcll(lo & hi & real);
+      hy += __popcll(~lo & hi & real);
+    }
+  int32_t* o = info + e * PE_NINFO;
+  o[PE_I_X] = s.x;
+  o[PE_I_Y] = s.y;
+  o[PE_I_THIRSTY] = th;
+  o[PE_I_HYDRATED] = hy;
+  o[PE_I_TOTAL_PLANTS] = th + hy;
+  o[PE_I_STEP] = s.step;
+  o[PE_I_EXPLORED] = s.expl;
+  o[PE_I_TOTAL_CELLS] = s.total;
+  o[PE_I_COLLIDED] = (s.flags & F_COLLIDED) ? 1 : 0;
+  o[PE_I_COLLISIONS] = s.coll;
+  o[PE_I_POISONED] = (int)((s.flags >> 2) & 7u);
+}
+
+// get_state: one thread per (env, cell).
+__global__ void pe_get_cells_kernel(StepArgs a, uint8_t* cells, int32_t* visits, int8_t* explored) {
+  const Geo& g = a.g;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)a.n * g.GG) return;
+  const int64_t e = t / g.GG;
+  const int c = (int)(t - e * g.GG);
+  const int row = c / g.G, col = c - row * g.G;
+  if (cells) cells[t] = (uint8_t)grid_code(a.st, g, e, row, col + g.R);
+  if (visits) visits[t] = a.st.v16[e * g.hstride + c];
+  if (explored) {
+    uint32_t w = a.st.expl[e * g.estride + (c >> 5)];
+    int8_t v = (w >> (c & 31)) & 1u ? 1 : 0;
+    if (v) {
+      Scal s = unpack(a.st.scal[e]);
+      if (s.x == row && s.y == col) v = 2;
+    }
+    explored[t] = v;
+  }
+}
+
+__global__ void pe_get_scal_kernel(StepArgs a, int32_t* scal) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.n) return;
+  Scal s = unpack(a.st.scal[e]);
+  int32_t* o = scal + e * PE_NSCAL;
+  o[PE_S_X] = s.x;
+  o[PE_S_Y] = s.y;
+  o[PE_S_STEP] = s.step;
+  o[PE_S_COLL] = s.coll;
+  o[PE_S_COLLIDED] = (s.flags & F_COLLIDED) ? 1 : 0;
+  o[PE_S_BONUS] = (s.flags & F_BONUS) ? 1 : 0;
+  o[PE_S_POISONED] = (int)((s.flags >> 2) & 7u);
+  o[PE_S_EPISODE] = (int32_t)s.episode;
+}
+
+// set_state (cells/visits): one thread per (env, row) rebuilds the packed rows.
+__global__ void pe_set_rows_kernel(StepArgs a, const uint8_t* cells, const int32_t* visits) {
+  const Geo& g = a.g;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)a.n * g.G) return;
+  const int64_t e = t / g.G;
+  const int row = (int)(t - e * g.G);
+  if (cells) {
+    for (int w = 0; w < g.WPR; ++w) a.st.grid[e * g.gstride + (int64_t)row * g.WPR + w] = a.st.tab->grid_pad[w];
+    for (int col = 0; col < g.G; ++col) {
+      int code = cells[e * g.GG + row * g.G + col] & 3;
+      if (code) grid_set(a.st, g, e, row, col + g.R, code);
+    }
+  }
+  if (visits) {
+    for (int w = 0; w < g.NW; ++w) a.st.vis[e * g.vstride + (int64_t)row * g.NW + w] = a.st.tab->vis_pad[w];
+    for (int col = 0; col < g.G; ++col) {
+      int32_t v = visits[e * g.GG + row * g.G + col];
+      uint32_t vc = v <= 0 ? 0u : (v >= 65535 ? 65535u : (uint32_t)v);
+      a.st.v16[e * g.hstride + row * g.G + col] = (uint16_t)vc;
+      vis_set(a.st, g, e, row, col, vc < 15u ? vc : 15u);
+    }
+  }
+}
+
+// set_state (explored bitmap + scalars + derived counters): one thread per env.
+__global__ void pe_set_env_kernel(StepArgs a, const int8_t* explored, const int32_t* scal) {
+  const Geo& g = a.g;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.n) return;
+  if (explored) {
+    for (int w = 0; w < g.estride; ++w) {
+      uint32_t bits = 0;
+      for (int b = 0; b < 32; ++b) {
+        int c = w * 32 + b;
+        if (c < g.GG && explored[e * g.GG + c] > 0) bits |= 1u << b;
+      }
+      a.st.expl[e * g.estride + w] = bits;
+    }
+  }
+  Scal s = unpack(a.st.scal[e]);
+  if (scal) {
+    const int32_t* i = scal + e * PE_NSCAL;
+    s.x = i[PE_S_X];
+    s.y = i[PE_S_Y];
+    s.step = i[PE_S_STEP] < 0 ? 0 : (i[PE_S_STEP] > 65535 ? 65535 : i[PE_S_STEP]);
+    s.coll = i[PE_S_COLL] < 0 ? 0 : (i[PE_S_COLL] > 65535 ? 65535 : i[PE_S_COLL]);
+    s.flags = (i[PE_S_COLLIDED] ? F_COLLIDED : 0u) | (i[PE_S_BONUS] ? F_BONUS : 0u) |
+              ((uint32_t)(i[PE_S_POISONED] & 7) << 2);
+    s.episode = (uint32_t)i[PE_S_EPISODE];
+  }
+  int ex = 0, ob = 0;
+  for (int w = 0; w < g.estride; ++w) ex += __popc(a.st.expl[e * g.estride + w]);
+  for (int row = 0; row < g.G; ++row)
+    for (int w = 0; w < g.WPR; ++w) {
+      uint64_t v = a.st.grid[e * g.gstride + (int64_t)row * g.WPR + w];
+      ob += __popcll(v & ~(v >> 1) & a.st.tab->grid_real[w] & kEven64);
+    }
+  s.expl = ex;
+  s.total = g.GG - ob;
+  a.st.scal[e] = pack(s);
+}
+
+__global__ void pe_synth_kernel(int n, uint64_t seed, uint32_t env_off, uint32_t t, int32_t* actions) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  uint4 o = philox(make_uint4(t, env_off + (uint32_t)e, 0u, kDomainAction), (uint32_t)seed, (uint32_t)(seed >> 32));
+  actions[e] = (int32_t)(o.x % 5u);
+}
+
+}  // namespace
+
+// ====================================================================== host side
+struct pe_handle {
+  int device;
+  int n;
+  pe_config cfg;
+  Geo g;
+  Rules rl;
+  State st;
+  void* mem;
+  size_t bytes;
+  int variant;
+  const char* kname;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(PE_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define PE_HIP(call)                                   \
+  do {                                                 \
+    hipError_t _e = (call);                            \
+    if (_e != hipSuccess) return hip_fail(_e, #call);  \
+  } while (0)
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+int bind_device(const pe_handle* h) {
+  int cur = -1;
+  PE_HIP(hipGetDevice(&cur));
+  if (cur != h->device) PE_HIP(hipSetDevice(h->device));
+  return PE_OK;
+}
+
+StepArgs base_args(const pe_handle* h) {
+  StepArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.st = h->st;
+  a.g = h->g;
+  a.rl = h->rl;
+  a.n = h->n;
+  a.autoreset = h->cfg.autoreset;
+  return a;
+}
+
+size_t lds_bytes(const Geo& g) { return sizeof(float) * (size_t)(kTabFloats + kBlock * g.DS); }
+
+enum Variant { V_GENERIC = 0, V_C16R6_1W = 1, V_C16R6 = 2, V_C64R6 = 3 };
+
+int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
+  dim3 grid((unsigned)((h->n + kBlock - 1) / kBlock)), block(kBlock);
+  size_t lds = lds_bytes(h->g);
+  switch (h->variant) {
+    case V_C16R6_1W: hipLaunchKernelGGL((pe_step_kernel<16, 6, true>), grid, block, lds, s, a); break;
+    case V_C16R6: hipLaunchKernelGGL((pe_step_kernel<16, 6, false>), grid, block, lds, s, a); break;
+    case V_C64R6: hipLaunchKernelGGL((pe_step_kernel<64, 6, false>), grid, block, lds, s, a); break;
+    default: hipLaunchKernelGGL((pe_step_kernel<0, 0, false>), grid, block, lds, s, a); break;
+  }
+  PE_HIP(hipGetLastError());
+  return PE_OK;
+}
+
+int launch_reset(const pe_handle* h, const StepArgs& a, hipStream_t s) {
+  dim3 grid((unsigned)((h->n + kBlock - 1) / kBlock)), block(kBlock);
+  size_t lds = lds_bytes(h->g);
+  switch (h->variant) {
+    case V_C16R6_1W: hipLaunchKernelGGL((pe_reset_kernel<16, 6, true>), grid, block, lds, s, a); break;
+    case V_C16R6: hipLaunchKernelGGL((pe_reset_kernel<16, 6, false>), grid, block, lds, s, a); break;
+    case V_C64R6: hipLaunchKernelGGL((pe_reset_kernel<64, 6, false>), grid, block, lds, s, a); break;
+    default: hipLaunchKernelGGL((pe_reset_kernel<0, 0, false>), grid, block, lds, s, a); break;
+  }
+  PE_HIP(hipGetLastError());
+  return PE_OK;
+}
+
+template <int C, int R>
+bool table_matches(const int8_t* dx, const int8_t* dy) {
+  for (int i = 0; i < C; ++i)
+    for (int r = 0; r < R; ++r)
+      if (LidarTab<C, R>::dx[i][r] != dx[i * R + r] || LidarTab<C, R>::dy[i][r] != dy[i * R + r]) return false;
+  return true;
+}
+
+const char* variant_name(int v) {
+  switch (v) {
+    case V_C16R6_1W: return "pe_step_kernel<C16,R6,1word>";
+    case V_C16R6: return "pe_step_kernel<C16,R6>";
+    case V_C64R6: return "pe_step_kernel<C64,R6>";
+    default: return "pe_step_kernel<generic>";
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+void pe_default_config(pe_config* c, int32_t G, int32_t P, int32_t O, int32_t R, int32_t C) {
+  std::memset(c, 0, sizeof(*c));
+  c->abi_version = PE_ABI_VERSION;
+  c->grid_size = G;
+  c->num_plants = P;
+  c->num_obstacles = O;
+  c->lidar_range = R;
+  c->lidar_channels = C;
+  c->max_steps = 1000;             // plantos_env.py:120
+  c->autoreset = 1;                // DummyVecEnv semantics
+  c->thirsty_plant_prob = 0.7;     // plantos_env.py:26
+  c->r_goal = 20;                  // plantos_env.py:76-83
+  c->r_mistake = -10;
+  c->r_invalid = -5;
+  c->r_water_empty = -5;
+  c->r_step = -0.1;
+  c->r_exploration = 10;
+  c->r_revisit = -1;
+  c->r_complete = 50;
+  c->seed = 0;
+  c->env_id_offset = 0;
+}
+
+int32_t pe_obs_dim(const pe_config* c) { return c->lidar_channels * 5 + 2 + 25; }
+
+const char* pe_last_error(void) { return g_err.c_str(); }
+
+int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** out) {
+  if (!c || !out) return fail(PE_ERR_ARG, "null argument");
+  *out = nullptr;
+  if (c->abi_version != PE_ABI_VERSION) return fail(PE_ERR_ARG, "ABI version mismatch");
+  const int G = c->grid_size, R = c->lidar_range, C = c->lidar_channels, P = c->num_plants, O = c->num_obstacles;
+  if (G < 1 || G > 128) return fail(PE_ERR_ARG, "grid_size must be in [1, 128]");
+  if (R < 1 || R > 64) return fail(PE_ERR_ARG, "lidar_range must be in [1, 64]");
+  if (C < 1 || C > 256) return fail(PE_ERR_ARG, "lidar_channels must be in [1, 256]");
+  if (P < 0 || P >= G * G) return fail(PE_ERR_ARG, "num_plants must be in [0, G*G)");
+  if (O < 0) return fail(PE_ERR_ARG, "num_obstacles must be >= 0");
+  if (O / 3 > 0 && G < 5) return fail(PE_ERR_ARG, "randint(2, G-3) needs grid_size >= 5 (plantos_env.py:344)");
+  if (c->max_steps < 1 || c->max_steps > 65535) return fail(PE_ERR_ARG, "max_steps must be in [1, 65535]");
+  if (n_envs < 1) return fail(PE_ERR_ARG, "n_envs must be >= 1");
+  if (2 * (G + 2 * R) > 64 * kMaxWPR) return fail(PE_ERR_ARG, "G + 2R too large");
+
+  int ndev = 0;
+  hipError_t he = hipGetDeviceCount(&ndev);
+  if (he != hipSuccess || ndev == 0) return fail(PE_ERR_DEVICE, "no HIP device available (no CPU fallback)");
+  if (device < 0 || device >= ndev) return fail(PE_ERR_ARG, "bad device index");
+  PE_HIP(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  PE_HIP(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(PE_ERR_DEVICE, std::string("built for gfx950, device is ") + prop.gcnArchName);
+
+  pe_handle* h = new (std::nothrow) pe_handle();
+  if (!h) return fail(PE_ERR_NOMEM, "host allocation failed");
+  h->device = device;
+  h->n = n_envs;
+  h->cfg = *c;
+  Geo& g = h->g;
+  g.G = G;
+  g.C = C;
+  g.R = R;
+  g.D = 5 * C + 27;
+  g.DS = g.D | 1;
+  g.GG = G * G;
+  g.WPR = (2 * (G + 2 * R) + 63) / 64;
+  g.NW = (4 * (G + 4) + 31) / 32 + 1;
+  g.EW = (g.GG + 31) / 32;
+  g.gstride = (int64_t)G * g.WPR;
+  g.vstride = (int64_t)G * g.NW;
+  g.hstride = (int64_t)align_up((size_t)g.GG, 8);
+  g.estride = (int64_t)align_up((size_t)g.EW, 4);
+  if (lds_bytes(g) > 160 * 1024) {
+    delete h;
+    return fail(PE_ERR_ARG, "observation tile does not fit LDS");
+  }
+
+  Rules& rl = h->rl;
+  rl.r_goal = c->r_goal;
+  rl.r_mistake = c->r_mistake;
+  rl.r_invalid = c->r_invalid;
+  rl.r_water_empty = c->r_water_empty;
+  rl.r_step = c->r_step;
+  rl.r_exploration = c->r_exploration;
+  rl.r_revisit = c->r_revisit;
+  rl.r_complete = c->r_complete;
+  rl.p_thirsty = c->thirsty_plant_prob;
+  rl.seed = c->seed;
+  rl.env_off = c->env_id_offset;
+  rl.P = P;
+  rl.O = O;
+  rl.max_steps = c->max_steps;
+
+  // host tables
+  Tables tab;
+  std::memset(&tab, 0, sizeof(tab));
+  for (int r = 0; r <= R; ++r) tab.dist[r] = (float)((double)r / (double)R);
+  for (int x = 0; x < G; ++x) tab.pos[x] = (float)((double)x / (double)G);
+  for (int v = 0; v < 16; ++v) tab.vis[v] = (float)((double)(v < 10 ? v : 10) / 10.0);
+  for (int p = 0; p < G + 2 * R; ++p) {
+    int w = (2 * p) / 64, b = (2 * p) % 64;
+    if (p < R || p >= G + R)
+      tab.grid_pad[w] |= 1ull << b;
+    else
+      tab.grid_real[w] |= 1ull << b;
+  }
+  for (int p = 0; p < G + 4; ++p)
+    if (p < 2 || p >= G + 2) tab.vis_pad[(4 * p) / 32] |= 10u << ((4 * p) % 32);
+  const size_t nl = (size_t)C * R;
+  int8_t* ldx = new int8_t[nl];
+  int8_t* ldy = new int8_t[nl];
+  const double pi = 3.141592653589793;  // math.pi; plantos_env.py:261-267
+  for (int i = 0; i < C; ++i) {
+    double angle = ((2.0 * pi) * (double)i) / (double)C;
+    for (int r = 1; r <= R; ++r) {
+      ldx[i * R + r - 1] = (int8_t)(int)((double)r * std::cos(angle));
+      ldy[i * R + r - 1] = (int8_t)(int)((double)r * std::sin(angle));
+    }
+  }
+  h->variant = V_GENERIC;
+  if (C == 16 && R == 6 && table_matches<16, 6>(ldx, ldy)) h->variant = g.WPR == 1 ? V_C16R6_1W : V_C16R6;
+  if (C == 64 && R == 6 && table_matches<64, 6>(ldx, ldy)) h->variant = V_C64R6;
+  h->kname = variant_name(h->variant);
+
+  // one device allocation carved into 256-B aligned arrays
+  const size_t n = (size_t)n_envs;
+  size_t off = 0;
+  auto carve = [&](size_t bytes) {
+    size_t o = off;
+    off = align_up(off + bytes, 256);
+    return o;
+  };
+  const size_t o_tab = carve(sizeof(Tables));
+  const size_t o_ldx = carve(nl), o_ldy = carve(nl);
+  const size_t o_err = carve(sizeof(uint32_t));
+  const size_t o_scal = carve(n * sizeof(uint4));
+  const size_t o_ret = carve(n * sizeof(double));
+  const size_t o_grid = carve(n * (size_t)g.gstride * 8);
+  const size_t o_vis = carve(n * (size_t)g.vstride * 4);
+  const size_t o_v16 = carve(n * (size_t)g.hstride * 2);
+  const size_t o_expl = carve(n * (size_t)g.estride * 4);
+  h->bytes = off;
+  hipError_t me = hipMalloc(&h->mem, h->bytes);
+  if (me != hipSuccess) {
+    delete[] ldx;
+    delete[] ldy;
+    delete h;
+    return fail(PE_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(me));
+  }
+  char* base = static_cast<char*>(h->mem);
+  h->st.tab = reinterpret_cast<const Tables*>(base + o_tab);
+  h->st.ldx = reinterpret_cast<const signed char*>(base + o_ldx);
+  h->st.ldy = reinterpret_cast<const signed char*>(base + o_ldy);
+  h->st.err_bits = reinterpret_cast<uint32_t*>(base + o_err);
+  h->st.scal = reinterpret_cast<uint4*>(base + o_scal);
+  h->st.ep_ret = reinterpret_cast<double*>(base + o_ret);
+  h->st.grid = reinterpret_cast<uint64_t*>(base + o_grid);
+  h->st.vis = reinterpret_cast<uint32_t*>(base + o_vis);
+  h->st.v16 = reinterpret_cast<uint16_t*>(base + o_v16);
+  h->st.expl = reinterpret_cast<uint32_t*>(base + o_expl);
+  int rc = PE_OK;
+  hipError_t e1 = hipMemset(h->mem, 0, h->bytes);
+  hipError_t e2 = hipMemcpy(base + o_tab, &tab, sizeof(Tables), hipMemcpyHostToDevice);
+  hipError_t e3 = hipMemcpy(base + o_ldx, ldx, nl, hipMemcpyHostToDevice);
+  hipError_t e4 = hipMemcpy(base + o_ldy, ldy, nl, hipMemcpyHostToDevice);
+  delete[] ldx;
+  delete[] ldy;
+  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess) {
+    (void)hipFree(h->mem);
+    delete h;
+    return fail(PE_ERR_DEVICE, "initial upload failed");
+  }
+  // every env starts reset (episode 0), like DummyVecEnv.reset() before the first step
+  StepArgs a = base_args(h);
+  rc = launch_reset(h, a, nullptr);
+  if (rc == PE_OK) {
+    hipError_t se = hipDeviceSynchronize();
+    if (se != hipSuccess) rc = hip_fail(se, "initial reset");
+  }
+  if (rc != PE_OK) {
+    (void)hipFree(h->mem);
+    delete h;
+    return rc;
+  }
+  *out = h;
+  return PE_OK;
+}
+
+int pe_destroy(pe_handle* h) {
+  if (!h) return PE_OK;
+  int rc = bind_device(h);
+  if (rc == PE_OK && h->mem) {
+    hipError_t e = hipFree(h->mem);
+    if (e != hipSuccess) rc = hip_fail(e, "hipFree");
+  }
+  delete h;
+  return rc;
+}
+
+int pe_seed(pe_handle* h, uint64_t seed, int32_t reset_episode_counters) {
+  if (!h) return fail(PE_ERR_ARG, "null handle");
+  h->rl.seed = seed;
+  h->cfg.seed = seed;
+  if (reset_episode_counters) {
+    int rc = bind_device(h);
+    if (rc) return rc;
+    // the episode counter is the 4th word of each packed scalar record
+    PE_HIP(hipMemset2D(reinterpret_cast<char*>(h->st.scal) + 12, sizeof(uint4), 0, 4, (size_t)h->n));
+  }
+  return PE_OK;
+}
+
+int pe_reset(pe_handle* h, const uint8_t* mask, float* obs, void* stream) {
+  if (!h) return fail(PE_ERR_ARG, "null handle");
+  int rc = bind_device(h);
+  if (rc) return rc;
+  StepArgs a = base_args(h);
+  a.mask = mask;
+  a.obs = obs;
+  return launch_reset(h, a, static_cast<hipStream_t>(stream));
+}
+
+int pe_step(pe_handle* h, const void* actions, int32_t action_bytes, float* obs, float* reward, uint8_t* terminated,
+            uint8_t* truncated, float* terminal_obs, double* ep_ret, int32_t* ep_len, void* stream) {
+  if (!h || !actions || !obs || !reward || !terminated || !truncated) return fail(PE_ERR_ARG, "null argument");
+  if (action_bytes != 4 && action_bytes != 8) return fail(PE_ERR_ARG, "action_bytes must be 4 or 8");
+  int rc = bind_device(h);
+  if (rc) return rc;
+  StepArgs a = base_args(h);
+  a.act_bytes = action_bytes;
+  a.actions = actions;
+  a.obs = obs;
+  a.reward = reward;
+  a.term = terminated;
+  a.trunc = truncated;
+  a.tobs = terminal_obs;
+  a.ep_ret_out = ep_ret;
+  a.ep_len_out = ep_len;
+  return launch_step(h, a, static_cast<hipStream_t>(stream));
+}
+
+int pe_get_info(pe_handle* h, int32_t* info, void* stream) {
+  if (!h || !info) return fail(PE_ERR_ARG, "null argument");
+  int rc = bind_device(h);
+  if (rc) return rc;
+  StepArgs a = base_args(h);
+  hipLaunchKernelGGL(pe_info_kernel, dim3((h->n + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream), a, info);
+  PE_HIP(hipGetLastError());
+  return PE_OK;
+}
+
+int pe_get_state(pe_handle* h, uint8_t* cells, int32_t* visits, int8_t* explored, int32_t* scalars, void* stream) {
+  if (!h) return fail(PE_ERR_ARG, "null handle");
+  int rc = bind_device(h);
+  if (rc) return rc;
+  StepArgs a = base_args(h);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (cells || visits || explored) {
+    int64_t total = (int64_t)h->n * h->g.GG;
+    hipLaunchKernelGGL(pe_get_cells_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a, cells, visits,
+                       explored);
+    PE_HIP(hipGetLastError());
+  }
+  if (scalars) {
+    hipLaunchKernelGGL(pe_get_scal_kernel, dim3((h->n + 255) / 256), dim3(256), 0, s, a, scalars);
+    PE_HIP(hipGetLastError());
+  }
+  return PE_OK;
+}
+
+int pe_set_state(pe_handle* h, const uint8_t* cells, const int32_t* visits, const int8_t* explored,
+                 const int32_t* scalars, void* stream) {
+  if (!h) return fail(PE_ERR_ARG, "null handle");
+  int rc = bind_device(h);
+  if (rc) return rc;
+  StepArgs a = base_args(h);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (cells || visits) {
+    int64_t total = (int64_t)h->n * h->g.G;
+    hipLaunchKernelGGL(pe_set_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a, cells, visits);
+    PE_HIP(hipGetLastError());
+  }
+  hipLaunchKernelGGL(pe_set_env_kernel, dim3((h->n + 255) / 256), dim3(256), 0, s, a, explored, scalars);
+  PE_HIP(hipGetLastError());
+  return PE_OK;
+}
+
+int pe_load_maps(pe_handle* h, int32_t k, const int32_t* env_index, const uint8_t* cells, const int32_t* rover,
+                 float* obs_k, void* stream) {
+  if (!h || (k > 0 && (!env_index || !cells || !rover))) return fail(PE_ERR_ARG, "null argument");
+  if (k <= 0) return PE_OK;
+  int rc = bind_device(h);
+  if (rc) return rc;
+  StepArgs a = base_args(h);
+  a.obs = obs_k;
+  hipLaunchKernelGGL(pe_load_maps_kernel, dim3((k + kBlock - 1) / kBlock), dim3(kBlock), lds_bytes(h->g),
+                     static_cast<hipStream_t>(stream), a, k, env_index, cells, rover);
+  PE_HIP(hipGetLastError());
+  return PE_OK;
+}
+
+int pe_synth_actions(pe_handle* h, uint64_t seed, uint32_t t, int32_t* actions, void* stream) {
+  if (!h || !actions) return fail(PE_ERR_ARG, "null argument");
+  int rc = bind_device(h);
+  if (rc) return rc;
+  hipLaunchKernelGGL(pe_synth_kernel, dim3((h->n + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream), h->n,
+                     seed, h->rl.env_off, t, actions);
+  PE_HIP(hipGetLastError());
+  return PE_OK;
+}
+
+int pe_poll_errors(pe_handle* h, int32_t* bits, void* stream) {
+  if (!h || !bits) return fail(PE_ERR_ARG, "null argument");
+  int rc = bind_device(h);
+  if (rc) return rc;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint32_t v = 0;
+  PE_HIP(hipMemcpyAsync(&v, h->st.err_bits, sizeof(v), hipMemcpyDeviceToHost, s));
+  PE_HIP(hipMemsetAsync(h->st.err_bits, 0, sizeof(uint32_t), s));
+  PE_HIP(hipStreamSynchronize(s));
+  *bits = (int32_t)((v >> 2) & 7u);
+  return PE_OK;
+}
+
+int32_t pe_num_envs(const pe_handle* h) { return h ? h->n : 0; }
+int32_t pe_kernel_variant(const pe_handle* h) { return h ? h->variant : -1; }
+const char* pe_kernel_name(const pe_handle* h) { return h ? h->kname : ""; }
+uint64_t pe_state_bytes(const pe_handle* h) { return h ? (uint64_t)h->bytes : 0; }
+
+}  // extern "C"

@@ -1,0 +1,190 @@
+"""PlantOSBatch: N PlantOS envs resident in HBM, driven through the C-ABI.
+
+torch is plumbing here: it owns the device buffers and supplies the HIP stream;
+all env work runs in the HIP kernels of libplantos_hip.so.
+"""
+import ctypes
+
+import torch
+
+from . import _capi as C
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class PlantOSBatch:
+    """A batch of `num_envs` independent PlantOS envs on one GPU.
+
+    Parameters mirror PlantOSEnv.__init__ (plantos_env.py:25-27) plus the batch
+    size, device, the device-rng seed, and `env_id_offset` (global id of env 0,
+    used when the batch is one shard of a multi-GPU job).
+    """
+
+    def __init__(self, num_envs, grid_size=21, num_plants=8, num_obstacles=50, lidar_range=2,
+                 lidar_channels=10, thirsty_plant_prob=0.7, max_steps=1000, autoreset=True, seed=0,
+                 env_id_offset=0, device=None, rewards=None):
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device() if torch.cuda.is_available() else 0)
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise C.PlantOSNativeError("PlantOSBatch needs a HIP device (no CPU fallback)")
+        L = C.lib()
+        cfg = C.default_config(grid_size, num_plants, num_obstacles, lidar_range, lidar_channels)
+        cfg.thirsty_plant_prob = float(thirsty_plant_prob)
+        cfg.max_steps = int(max_steps)
+        cfg.autoreset = int(bool(autoreset))
+        cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        cfg.env_id_offset = int(env_id_offset)
+        for k, v in (rewards or {}).items():
+            setattr(cfg, k, float(v))
+        self.cfg = cfg
+        self.num_envs = int(num_envs)
+        self.grid_size = grid_size
+        self.obs_dim = int(L.pe_obs_dim(ctypes.byref(cfg)))
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            C.check(L.pe_create(ctypes.byref(cfg), self.device.index or 0, self.num_envs, ctypes.byref(h)),
+                    "pe_create")
+        self._h = h
+        n, D, dev = self.num_envs, self.obs_dim, self.device
+        self.obs = torch.zeros((n, D), dtype=torch.float32, device=dev)
+        self.reward = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.terminated = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.truncated = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.terminal_obs = torch.zeros((n, D), dtype=torch.float32, device=dev)
+        self.episode_return = torch.zeros(n, dtype=torch.float64, device=dev)
+        self.episode_length = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.info_buf = torch.zeros((n, C.PE_NINFO), dtype=torch.int32, device=dev)
+        self.raise_on_errors()
+
+    def raise_on_errors(self):
+        """Surface the reference's exceptions that the batch records per env:
+        ValueError when a reset had no room (plantos_env.py:360-364)."""
+        bits = self.poll_errors()
+        if bits & 4:
+            raise ValueError("Not enough available positions to place the plants and the rover "
+                             "(plantos_env.py:360-364)")
+        return bits
+
+    # ----------------------------------------------------------------- plumbing
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    @property
+    def handle(self):
+        if not self._h:
+            raise ValueError("PlantOSBatch is closed")
+        return self._h
+
+    @property
+    def kernel_name(self):
+        return C.lib().pe_kernel_name(self.handle).decode()
+
+    @property
+    def kernel_variant(self):
+        return int(C.lib().pe_kernel_variant(self.handle))
+
+    @property
+    def state_bytes(self):
+        return int(C.lib().pe_state_bytes(self.handle))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            C.check(C.lib().pe_destroy(self._h), "pe_destroy")
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ----------------------------------------------------------------- hot path
+    def reset(self, mask=None, obs=None):
+        """Reset masked envs (all if mask is None); returns obs [n, D] (device)."""
+        out = self.obs if obs is None else obs
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+        with torch.cuda.device(self.device):
+            C.check(C.lib().pe_reset(self.handle, _ptr(m), _ptr(out), self._stream()), "pe_reset")
+        return out
+
+    def step(self, actions, obs=None, want_terminal_obs=True):
+        """One step of every env. `actions`: int32/int64 tensor [n] on the device
+        (other inputs are converted).  Returns device tensors
+        (obs, reward, terminated, truncated)."""
+        a = actions
+        if not (isinstance(a, torch.Tensor) and a.device == self.device and a.dtype in (torch.int32, torch.int64)):
+            a = torch.as_tensor(a).to(device=self.device, dtype=torch.int64)
+        a = a.contiguous()
+        if a.numel() != self.num_envs:
+            raise ValueError(f"expected {self.num_envs} actions, got {a.numel()}")
+        out = self.obs if obs is None else obs
+        with torch.cuda.device(self.device):
+            C.check(C.lib().pe_step(self.handle, _ptr(a), a.element_size(), _ptr(out), _ptr(self.reward),
+                                    _ptr(self.terminated), _ptr(self.truncated),
+                                    _ptr(self.terminal_obs) if want_terminal_obs else None,
+                                    _ptr(self.episode_return), _ptr(self.episode_length), self._stream()),
+                    "pe_step")
+        return out, self.reward, self.terminated, self.truncated
+
+    # ----------------------------------------------------------------- inspection
+    def get_info(self):
+        with torch.cuda.device(self.device):
+            C.check(C.lib().pe_get_info(self.handle, _ptr(self.info_buf), self._stream()), "pe_get_info")
+        return self.info_buf
+
+    def get_state(self):
+        """Canonical state in the reference's terms (plantos_env.py:96-123)."""
+        n, G = self.num_envs, self.grid_size
+        cells = torch.empty((n, G, G), dtype=torch.uint8, device=self.device)
+        visits = torch.empty((n, G, G), dtype=torch.int32, device=self.device)
+        explored = torch.empty((n, G, G), dtype=torch.int8, device=self.device)
+        scal = torch.empty((n, C.PE_NSCAL), dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            C.check(C.lib().pe_get_state(self.handle, _ptr(cells), _ptr(visits), _ptr(explored), _ptr(scal),
+                                         self._stream()), "pe_get_state")
+        return {"cells": cells, "visits": visits, "explored": explored, "scalars": scal}
+
+    def set_state(self, cells=None, visits=None, explored=None, scalars=None):
+        def dev(x, dt):
+            return None if x is None else torch.as_tensor(x).to(device=self.device, dtype=dt).contiguous()
+        c, v, e, s = dev(cells, torch.uint8), dev(visits, torch.int32), dev(explored, torch.int8), dev(
+            scalars, torch.int32)
+        with torch.cuda.device(self.device):
+            C.check(C.lib().pe_set_state(self.handle, _ptr(c), _ptr(v), _ptr(e), _ptr(s), self._stream()),
+                    "pe_set_state")
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def load_maps(self, env_index, cells, rover):
+        """Reset envs `env_index` to given layouts; returns their obs [k, D]."""
+        idx = torch.as_tensor(env_index).to(device=self.device, dtype=torch.int32).contiguous()
+        cl = torch.as_tensor(cells).to(device=self.device, dtype=torch.uint8).contiguous()
+        rv = torch.as_tensor(rover).to(device=self.device, dtype=torch.int32).contiguous()
+        k = idx.numel()
+        out = torch.empty((k, self.obs_dim), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            C.check(C.lib().pe_load_maps(self.handle, k, _ptr(idx), _ptr(cl), _ptr(rv), _ptr(out), self._stream()),
+                    "pe_load_maps")
+        return out
+
+    def synth_actions(self, seed, t, out=None):
+        out = torch.empty(self.num_envs, dtype=torch.int32, device=self.device) if out is None else out
+        with torch.cuda.device(self.device):
+            C.check(C.lib().pe_synth_actions(self.handle, int(seed), int(t), _ptr(out), self._stream()),
+                    "pe_synth_actions")
+        return out
+
+    def poll_errors(self):
+        bits = ctypes.c_int32(0)
+        with torch.cuda.device(self.device):
+            C.check(C.lib().pe_poll_errors(self.handle, ctypes.byref(bits), self._stream()), "pe_poll_errors")
+        return int(bits.value)
+
+    def seed(self, seed, reset_episode_counters=True):
+        C.check(C.lib().pe_seed(self.handle, int(seed) & 0xFFFFFFFFFFFFFFFF, int(bool(reset_episode_counters))),
+                "pe_seed")
+        self.cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF

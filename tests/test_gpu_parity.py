@@ -1,0 +1,281 @@
+"""GPU parity: the HIP hot path (through the C-ABI) vs the oracle / reference fixtures.
+
+Bar: bit-exact integer state and obs; reward bit-exact to float32(reference f64)
+(tolerance 0 -- stricter than north_star's 1e-6); episode returns bit-exact f64.
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import INJECT_CFGS, TRAJ_FILES, cfg_tuple, load
+from oracle import oracle as O
+from oracle_rollout import OracleVec
+
+pytestmark = pytest.mark.gpu
+
+CFG = {
+    "g20": (20, 10, 12, 6, 16),
+    "g21": (21, 8, 50, 2, 10),
+    "g25": (25, 10, 12, 6, 16),
+    "g64": (64, 100, 120, 6, 64),
+    "g64r32": (64, 100, 120, 32, 64),
+    "g7": (7, 3, 3, 3, 12),
+    "g32": (32, 20, 30, 9, 24),
+}
+
+
+def make(cfg, n, **kw):
+    from plantos_amd import PlantOSBatch
+    G, P, Ob, R, C = cfg
+    return PlantOSBatch(n, grid_size=G, num_plants=P, num_obstacles=Ob, lidar_range=R, lidar_channels=C,
+                        device="cuda:0", **kw)
+
+
+def np_(t):
+    return t.detach().cpu().numpy()
+
+
+@pytest.mark.parametrize("name", INJECT_CFGS)
+def test_injected_step_parity(name):
+    f = load(f"inject_{name}")
+    cfg = cfg_tuple(f)
+    n = f["cells"].shape[0]
+    b = make(cfg, n, autoreset=False)
+    scal = np.zeros((n, 8), np.int32)
+    scal[:, :6] = f["scal"]
+    b.set_state(cells=f["cells"], visits=f["visits"].astype(np.int32), explored=f["explored"], scalars=scal)
+    obs_pre = np_(b.reset(mask=np.zeros(n, np.uint8)))
+    assert (obs_pre == f["obs_pre"]).all()
+    obs, rew, te, tr = b.step(torch.as_tensor(f["action"], dtype=torch.int32, device="cuda:0"))
+    assert (np_(obs) == f["obs"]).all()
+    assert (np_(rew) == f["reward"].astype(np.float32)).all()
+    assert (np_(te).astype(bool) == f["term"].astype(bool)).all()
+    assert (np_(tr).astype(bool) == f["trunc"].astype(bool)).all()
+    st = b.get_state()
+    assert (np_(st["cells"]) == f["cells_post"]).all()
+    assert (np_(st["visits"]) == f["visits_post"].astype(np.int32)).all()
+    assert (np_(st["explored"]) == f["explored_post"]).all()
+    sp = f["scal_post"]
+    s = np_(st["scalars"])
+    assert (s[:, :6] == sp[:, :6]).all()
+    assert ((s[:, 6] & 1).astype(bool) == f["root_raises"].astype(bool)).all()
+    info = np_(b.get_info())
+    from plantos_amd import _capi as C
+    assert (info[:, C.PE_I_EXPLORED] == sp[:, 6]).all()
+    assert (info[:, C.PE_I_TOTAL_CELLS] == sp[:, 7]).all()
+    assert (info[:, C.PE_I_THIRSTY] == sp[:, 8]).all()
+    assert (info[:, C.PE_I_HYDRATED] == sp[:, 9]).all()
+    b.close()
+
+
+def test_kat_seed0_gpu():
+    """Appendix B through the GPU: reference map loaded, 1000 reference actions."""
+    k = load("kat_seed0")
+    b = make(cfg_tuple(k), 1)
+    obs0 = np_(b.load_maps([0], k["cells0"][None], k["rover0"][None]))
+    assert (obs0[0] == k["obs"][0]).all()
+    acts = torch.as_tensor(k["actions"], dtype=torch.int64, device="cuda:0")
+    for t in range(1000):
+        obs, rew, te, tr = b.step(acts[t:t + 1])
+        assert float(np_(rew)[0]) == np.float32(k["reward"][t]), t
+        assert bool(np_(te)[0]) == bool(k["terminated"][t]) and bool(np_(tr)[0]) == bool(k["truncated"][t]), t
+        if t < 999:
+            assert (np_(obs)[0] == k["obs"][t + 1]).all(), t
+    # step 1000 truncates: terminal obs is the reference's final obs, return is the f64 sum
+    assert (np_(b.terminal_obs)[0] == k["obs"][1000]).all()
+    assert float(np_(b.episode_return)[0]) == float(k["reward_sum"])
+    assert int(np_(b.episode_length)[0]) == 1000
+    b.close()
+
+
+@pytest.mark.parametrize("name", TRAJ_FILES)
+def test_dummyvecenv_trajectory_gpu(name):
+    """Reference DummyVecEnv rollouts; reset layouts supplied from the fixture
+    (CPython-stream mode), everything else computed on the GPU."""
+    f = load(name)
+    acts = f["actions"]
+    T, N = acts.shape
+    b = make(cfg_tuple(f), N)
+    obs0 = np_(b.load_maps(np.arange(N), f["maps0"], f["rover0"]))
+    assert (obs0 == f["obs0"]).all()
+    ri = 0
+    for t in range(T):
+        obs, rew, te, tr = b.step(torch.as_tensor(acts[t], device="cuda:0"))
+        obs = np_(obs).copy()
+        assert (np_(rew) == f["reward"][t].astype(np.float32)).all(), t
+        te_, tr_ = np_(te).astype(bool), np_(tr).astype(bool)
+        assert (te_ == f["terminated"][t].astype(bool)).all() and (tr_ == f["truncated"][t].astype(bool)).all()
+        done = np.nonzero(te_ | tr_)[0]
+        if len(done):
+            tobs = np_(b.terminal_obs)
+            for e in done:
+                assert (tobs[e] == f["terminal_obs"][t, e]).all()
+            sel = np.arange(ri, ri + len(done))
+            assert (f["reset_t"][sel] == t).all() and (f["reset_env"][sel] == done).all()
+            fresh = np_(b.load_maps(done, f["reset_cells"][sel], f["reset_rover"][sel]))
+            obs[done] = fresh
+            ri += len(done)
+        assert (obs == f["obs"][t]).all(), t
+    b.close()
+
+
+@pytest.mark.parametrize("name", ["g20", "g21", "g64", "g7", "g32", "g64r32"])
+def test_device_reset_matches_oracle_philox(name):
+    cfg = CFG[name]
+    n = 512 if cfg[0] <= 32 else 128
+    b = make(cfg, n, seed=1234)
+    st = {k: np_(v) for k, v in b.get_state().items()}
+    ob = O.Batch(O.config(*cfg), n)
+    for e in range(n):
+        ob.reset_philox(e, 1234, e, 0)
+    assert (st["cells"] == ob.cells).all()
+    assert (st["visits"] == ob.visits).all()
+    assert (st["explored"] == ob.explored).all()
+    assert (st["scalars"] == ob.scal).all()
+    assert (np_(b.reset(mask=np.zeros(n, np.uint8))) == ob.obs()).all()
+    b.close()
+
+
+@pytest.mark.parametrize("name,n,steps", [("g20", 4096, 1100), ("g21", 1000, 300), ("g7", 777, 400),
+                                          ("g64", 256, 120), ("g64r32", 96, 60), ("g25", 300, 200)])
+def test_rollout_parity_device_rng(name, n, steps):
+    """Device-rng episodes with synthetic actions, auto-reset included (g20 crosses
+    the 1000-step truncation): every output of every step vs the oracle."""
+    cfg = CFG[name]
+    seed = 77
+    b = make(cfg, n, seed=seed)
+    ov = OracleVec(cfg, np.arange(n), seed)
+    assert (np_(b.reset(mask=np.zeros(n, np.uint8))) == ov.obs()).all()
+    act = torch.empty(n, dtype=torch.int32, device="cuda:0")
+    for t in range(steps):
+        b.synth_actions(seed, t, out=act)
+        a_np = np_(act)
+        if t == 0:
+            assert all(a_np[e] == O.synth_action(seed, e, 0) for e in range(0, n, max(1, n // 50)))
+        obs, rew, te, tr = b.step(act)
+        o_obs, o_rew, o_te, o_tr, o_tobs, o_ret, o_len = ov.step(a_np)
+        assert (np_(rew) == o_rew.astype(np.float32)).all(), t
+        assert (np_(te).astype(bool) == o_te).all() and (np_(tr).astype(bool) == o_tr).all(), t
+        assert (np_(obs) == o_obs).all(), t
+        done = o_te | o_tr
+        if done.any():
+            assert (np_(b.terminal_obs)[done] == o_tobs[done]).all()
+            assert (np_(b.episode_return)[done] == o_ret[done]).all()
+            assert (np_(b.episode_length)[done] == o_len[done]).all()
+    st = b.get_state()
+    assert (np_(st["visits"]) == ov.b.visits).all()
+    assert (np_(st["cells"]) == ov.b.cells).all()
+    assert (np_(st["scalars"]) == ov.b.scal).all()
+    b.close()
+
+
+def test_headline_size_sampled_parity_and_invariants():
+    """65536 envs (BASELINE headline) for 1100 steps: oracle replays a sample of
+    global env ids (envs are independent), plus size-independent invariants."""
+    cfg = CFG["g20"]
+    n, seed, steps = 65536, 5, 1100
+    b = make(cfg, n, seed=seed)
+    sample = np.r_[0:64, 30000:30064, 65472:65536]
+    ov = OracleVec(cfg, sample, seed)
+    act = torch.empty(n, dtype=torch.int32, device="cuda:0")
+    total_ret = torch.zeros(n, dtype=torch.float64, device="cuda:0")
+    for t in range(steps):
+        b.synth_actions(seed, t, out=act)
+        obs, rew, te, tr = b.step(act)
+        o_obs, o_rew, o_te, o_tr, *_ = ov.step(np_(act)[sample])
+        if t % 50 == 0 or t in (999, 1000):
+            ob = np_(obs)
+            assert (ob[sample] == o_obs).all(), t
+            assert (np_(rew)[sample] == o_rew.astype(np.float32)).all(), t
+            # invariants: one-hot per ray, distances in {r/R}, visit slice in {k/10}
+            lid = ob[:, :80].reshape(n, 16, 5)
+            assert (lid[:, :, 1:].sum(-1) == 1.0).all()
+            assert np.isin(lid[:, :, 0], np.float32(np.arange(1, 7) / 6.0)).all()
+            assert np.isin(ob[:, 82:], np.float32(np.arange(11) / 10.0)).all()
+        total_ret += rew.double()
+    assert (np_(tr)[sample] == o_tr).all()
+    st = b.get_state()
+    s = np_(st["scalars"])
+    assert (s[sample] == ov.b.scal).all()
+    # every env truncated exactly once at step 1000 (random policy never finishes)
+    assert (s[:, 7] == 2).all() and (s[:, 2] == 100).all()
+    b.close()
+
+
+def test_determinism_and_sharding_equivalence():
+    """Same seed => identical outputs; two shards with env_id_offset reproduce one big batch."""
+    cfg = CFG["g20"]
+    n = 4096
+    full = make(cfg, n, seed=9)
+    lo = make(cfg, n // 2, seed=9, env_id_offset=0)
+    hi = make(cfg, n // 2, seed=9, env_id_offset=n // 2)
+    act = torch.empty(n, dtype=torch.int32, device="cuda:0")
+    for t in range(1005):
+        full.synth_actions(3, t, out=act)
+        o, r, _, _ = full.step(act)
+        o1, r1, _, _ = lo.step(act[: n // 2].clone())
+        o2, r2, _, _ = hi.step(act[n // 2:].clone())
+        if t % 100 == 0 or t > 995:
+            assert torch.equal(o[: n // 2], o1) and torch.equal(o[n // 2:], o2)
+            assert torch.equal(r[: n // 2], r1) and torch.equal(r[n // 2:], r2)
+    for x in (full, lo, hi):
+        x.close()
+
+
+@pytest.mark.parametrize("n", [1, 63, 65, 1000])
+def test_ragged_batch_sizes(n):
+    cfg = CFG["g20"]
+    b = make(cfg, n, seed=3)
+    ov = OracleVec(cfg, np.arange(n), 3)
+    for t in range(30):
+        a = np.array([O.synth_action(11, e, t) for e in range(n)], np.int64)
+        obs, rew, te, tr = b.step(torch.as_tensor(a, device="cuda:0"))  # int64 actions
+        o_obs, o_rew, *_ = ov.step(a)
+        assert (np_(obs) == o_obs).all() and (np_(rew) == o_rew.astype(np.float32)).all()
+    b.close()
+
+
+def test_out_of_range_actions():
+    """Negative actions wrap like Python list indices (plantos_env.py:187); < -4 is the
+    reference's IndexError, flagged (bit1); >= 4 waters (plantos_env.py:168-169)."""
+    cfg = CFG["g20"]
+    n = 64
+    b = make(cfg, n, seed=4, autoreset=False)
+    ov = OracleVec(cfg, np.arange(n), 4)
+    rng = np.random.default_rng(0)
+    for t in range(50):
+        a = rng.integers(-6, 9, n).astype(np.int64)
+        obs, rew, te, tr = b.step(torch.as_tensor(a, device="cuda:0"))
+        o_obs, o_rew, o_te, o_tr = ov.b.step(a)
+        assert (np_(obs) == o_obs).all() and (np_(rew) == o_rew.astype(np.float32)).all()
+    assert b.poll_errors() & 2
+    s = np_(b.get_state()["scalars"])
+    assert (s == ov.b.scal).all()
+    b.close()
+
+
+def test_no_room_raises():
+    from plantos_amd import PlantOSBatch
+    # G=5: one obstacle cluster of >= 4 cells leaves <= 21 free cells < 22 + 1
+    with pytest.raises(ValueError):
+        PlantOSBatch(8, grid_size=5, num_plants=22, num_obstacles=3, lidar_range=2, lidar_channels=4,
+                     device="cuda:0")
+
+
+def test_terminating_explorer_episode():
+    """Termination + completion bonus (plantos_env.py:176-181) on the GPU: a map
+    with one free cell left, then a move into it."""
+    cfg = CFG["g7"]
+    f = load("inject_g7")
+    idx = np.nonzero(f["term"])[0]
+    n = len(idx)
+    b = make(cfg, n, autoreset=True, seed=1)
+    scal = np.zeros((n, 8), np.int32)
+    scal[:, :6] = f["scal"][idx]
+    b.set_state(cells=f["cells"][idx], visits=f["visits"][idx].astype(np.int32), explored=f["explored"][idx],
+                scalars=scal)
+    obs, rew, te, tr = b.step(torch.as_tensor(f["action"][idx], device="cuda:0"))
+    assert np_(te).all()
+    assert (np_(rew) == f["reward"][idx].astype(np.float32)).all()
+    assert (np_(b.terminal_obs) == f["obs"][idx]).all()
+    b.close()
