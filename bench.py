@@ -114,18 +114,20 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     K = args.steps
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record()
     for k in range(K):
-        ev[k][0].record()
         one_step(args.warmup + k)
-        ev[k][1].record()
+    ev1.record()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(s.elapsed_time(e) for s, e in ev) / K  # per-launch device time (HIP events)
+    # average launch duration: HIP events on the launch stream over the timed region
+    # (back-to-back launches, so this includes the ~1-2 us inter-kernel boundary)
+    kern_ms = ev0.elapsed_time(ev1) / K
     if dist:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

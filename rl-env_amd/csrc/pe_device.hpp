@@ -140,11 +140,11 @@ struct Stream {
       ++blk;
       pos = 0;
     }
-    uint32_t v = buf[0];
-    // select without dynamic register indexing
-    v = pos == 1 ? buf[1] : v;
-    v = pos == 2 ? buf[2] : v;
-    v = pos == 3 ? buf[3] : v;
+    // mask select: a ternary chain over buf[] is folded into a dynamically
+    // indexed load, which would put the stream state in scratch memory
+    const uint32_t m0 = 0u - (uint32_t)(pos == 0), m1 = 0u - (uint32_t)(pos == 1);
+    const uint32_t m2 = 0u - (uint32_t)(pos == 2), m3 = 0u - (uint32_t)(pos == 3);
+    const uint32_t v = (buf[0] & m0) | (buf[1] & m1) | (buf[2] & m2) | (buf[3] & m3);
     ++pos;
     return v;
   }

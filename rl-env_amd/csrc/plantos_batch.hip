@@ -17,6 +17,7 @@
 #include "../../include/plantos_batch.h"
 #include "lidar_tables.inc"
 #include "pe_device.hpp"
+#include "pe_fast.hpp"
 
 using namespace pe;
 
@@ -75,75 +76,6 @@ __device__ __forceinline__ void build_obs_generic(const StepArgs& a, int64_t e, 
     int xr = x + lx - 2;
     uint32_t win = (xr >= 0 && xr < g.G) ? vis_window(a.st, g, e, xr, y) : 0xAAAAAu;
     for (int ly = 0; ly < 5; ++ly) row[5 * C + 2 + 5 * lx + ly] = tvis[(win >> (4 * ly)) & 15u];
-  }
-}
-
-// Specialized: compile-time (C, R) offsets; the (2R+1) window rows around the rover
-// are loaded once and every probe is a constant-shift 2-bit extract.
-template <int C, int R, bool ONEWORD>
-__device__ __forceinline__ void build_obs_static(const StepArgs& a, int64_t e, int x, int y, float* row,
-                                                 const float* tpos, const float* tvis) {
-  constexpr int W = 2 * R + 1;
-  static_assert(2 * W <= 64, "window must fit one u64");
-  const Geo& g = a.g;
-  const uint64_t* gbase = a.st.grid + e * g.gstride;
-  uint64_t win[W];
-  const int bit = 2 * y;
-#pragma unroll
-  for (int k = 0; k < W; ++k) {
-    int xr = x + k - R;
-    uint64_t v = kEven64;  // off-map row: every cell reads as obstacle
-    if (xr >= 0 && xr < g.G) {
-      if constexpr (ONEWORD) {
-        v = gbase[xr] >> bit;
-      } else {
-        const uint64_t* p = gbase + (int64_t)xr * g.WPR + (bit >> 6);
-        int o = bit & 63;
-        uint64_t lo = p[0];
-        uint64_t hi = ((bit >> 6) + 1 < g.WPR) ? p[1] : 0ull;
-        v = o ? ((lo >> o) | (hi << (64 - o))) : lo;
-      }
-    }
-    win[k] = v;
-  }
-  using T = LidarTab<C, R>;
-#pragma unroll
-  for (int i = 0; i < C; ++i) {
-    float dist = 1.0f;  // R/R
-    int ent = EMPTY;
-#pragma unroll
-    for (int r = R; r >= 1; --r) {
-      const int dx = T::dx[i][r - 1], dy = T::dy[i][r - 1];
-      int code = (int)((win[dx + R] >> (2 * (dy + R))) & 3u);
-      if (code != EMPTY) {
-        dist = (float)((double)r / (double)R);  // constant-folded: float(r/R), :288
-        ent = code;
-      }
-    }
-    row[5 * i] = dist;
-    row[5 * i + 1] = ent == 0 ? 1.0f : 0.0f;
-    row[5 * i + 2] = ent == 1 ? 1.0f : 0.0f;
-    row[5 * i + 3] = ent == 2 ? 1.0f : 0.0f;
-    row[5 * i + 4] = ent == 3 ? 1.0f : 0.0f;
-  }
-  row[5 * C] = tpos[x];
-  row[5 * C + 1] = tpos[y];
-#pragma unroll
-  for (int lx = 0; lx < 5; ++lx) {
-    int xr = x + lx - 2;
-    uint32_t w5 = (xr >= 0 && xr < g.G) ? vis_window(a.st, g, e, xr, y) : 0xAAAAAu;
-#pragma unroll
-    for (int ly = 0; ly < 5; ++ly) row[5 * C + 2 + 5 * lx + ly] = tvis[(w5 >> (4 * ly)) & 15u];
-  }
-}
-
-template <int VC, int VR, bool ONEWORD>
-__device__ __forceinline__ void build_obs(const StepArgs& a, int64_t e, int x, int y, float* row, const float* tdist,
-                                          const float* tpos, const float* tvis) {
-  if constexpr (VC == 0) {
-    build_obs_generic(a, e, x, y, row, tdist, tpos, tvis);
-  } else {
-    build_obs_static<VC, VR, ONEWORD>(a, e, x, y, row, tpos, tvis);
   }
 }
 
@@ -238,7 +170,6 @@ __device__ __forceinline__ void store_tile(const float* rows, float* dst, int va
 }
 
 // ------------------------------------------------------------------ kernels
-template <int VC, int VR, bool ONEWORD>
 __global__ __launch_bounds__(kBlock) void pe_step_kernel(StepArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* tdist = smem;
@@ -263,7 +194,7 @@ __global__ __launch_bounds__(kBlock) void pe_step_kernel(StepArgs a) {
     if ((term || trunc) && a.autoreset) {
       // DummyVecEnv.step_wait: keep the terminal obs, reset, return the reset obs.
       if (a.tobs) {
-        build_obs<VC, VR, ONEWORD>(a, e, s.x, s.y, row, tdist, tpos, tvis);
+        build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis);
         float* t = a.tobs + e * a.g.D;
         for (int k = 0; k < a.g.D; ++k) t[k] = row[k];
       }
@@ -274,15 +205,174 @@ __global__ __launch_bounds__(kBlock) void pe_step_kernel(StepArgs a) {
     }
     a.st.ep_ret[e] = ret;
     a.st.scal[e] = pack(s);
-    build_obs<VC, VR, ONEWORD>(a, e, s.x, s.y, row, tdist, tpos, tvis);
+    build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis);
   }
   __syncthreads();
   const int64_t valid = a.n - e0 < kBlock ? a.n - e0 : kBlock;
   store_tile(rows, a.obs + e0 * a.g.D, (int)valid, a.g.D, a.g.DS);
 }
 
+
+// Specialized fused step (compile-time C, R): two load rounds per lane, the rest
+// from registers (pe_fast.hpp).  Same semantics as pe_step_kernel + transition().
+template <int C, int R, bool ONEWORD>
+__global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* tpos = smem + 72;
+  float* tvis = smem + 328;
+  float* rows = smem + kTabFloats;
+  const Geo& g = a.g;
+  const Rules& rl = a.rl;
+  const State& st = a.st;
+  const int64_t e0 = (int64_t)blockIdx.x * kBlock;
+  const int64_t e = e0 + threadIdx.x;
+  const bool live = e < a.n;
+  float* row = rows + threadIdx.x * g.DS;
+  // ---- round 1: env-indexed loads
+  uint4 sw = make_uint4(0u, 0u, 0u, 0u);
+  int64_t action = 0;
+  double ret = 0.0;
+  if (live) {
+    sw = st.scal[e];
+    action = a.act_bytes == 8 ? reinterpret_cast<const int64_t*>(a.actions)[e]
+                              : (int64_t)reinterpret_cast<const int32_t*>(a.actions)[e];
+    ret = st.ep_ret[e];
+  }
+  load_tables(smem, st.tab);
+  __syncthreads();
+  if (live) {
+    Scal s = unpack(sw);
+    s.step = s.step < 65535 ? s.step + 1 : 65535;                  // plantos_env.py:162
+    bool mv = false, water = false;
+    int dxm = 0, dym = 0;
+    if (action < 4) {                                              // :166
+      const int64_t ai = action < 0 ? action + 4 : action;         // Python negative index
+      if (ai < 0) {
+        s.flags |= F_POISON_ACT;                                   // reference IndexError
+        atomicOr(st.err_bits, F_POISON_ACT);
+      } else {
+        mv = true;                                                 // :186 N,E,S,W
+        dxm = ai == 0 ? -1 : (ai == 2 ? 1 : 0);
+        dym = ai == 1 ? 1 : (ai == 3 ? -1 : 0);
+      }
+    } else {
+      water = true;
+    }
+    const int nx = s.x + dxm, ny = s.y + dym;
+    const bool inb = mv && nx >= 0 && nx < g.G && ny >= 0 && ny < g.G;
+    // ---- round 2: position-indexed loads
+    Window<R, ONEWORD> w;
+    w.load(st, g, e, s.x, s.y);
+    const int cell_o = s.x * g.G + s.y, cell_n = nx * g.G + ny;
+    uint16_t* vp = st.v16 + e * g.hstride + (inb ? cell_n : 0);
+    uint32_t* ep_o = st.expl + e * g.estride + (cell_o >> 5);
+    uint32_t* ep_n = st.expl + e * g.estride + ((inb ? cell_n : cell_o) >> 5);
+    uint32_t v = 0u, eo = 0u, en = 0u;
+    if (inb) {
+      v = *vp;
+      eo = *ep_o;
+      en = *ep_n;
+    }
+    double h = 0.0;
+    int dxv = 0;
+    if (mv) {
+      const bool ok = inb && w.code(dxm, ny) != OBST;              // :193-195
+      if (ok) {
+        const bool never = v == 0u;                                // :197
+        const uint32_t v1 = v < 65535u ? v + 1u : 65535u;          // :203
+        *vp = (uint16_t)v1;
+        const uint32_t nib = v1 < 15u ? v1 : 15u;
+        const int pb = 4 * (ny + 2) - 32 * ((4 * w.ybv) >> 5);
+        uint32_t* vrow = st.vis + e * g.vstride + (int64_t)nx * g.NW + ((4 * w.ybv) >> 5);
+#pragma unroll
+        for (int k = 2; k <= 4; ++k) {
+          if (k == 3 + dxm) {
+            if (pb < 32) {
+              w.vlo[k] = (w.vlo[k] & ~(0xFu << pb)) | (nib << pb);
+              vrow[0] = w.vlo[k];
+            } else {
+              w.vhi[k] = (w.vhi[k] & ~(0xFu << (pb - 32))) | (nib << (pb - 32));
+              vrow[1] = w.vhi[k];
+            }
+          }
+        }
+        const uint32_t bo = 1u << (cell_o & 31), bn = 1u << (cell_n & 31);
+        if ((cell_o >> 5) == (cell_n >> 5)) {                      // explored[old]=1, [new]=2 (:198-200)
+          uint32_t wv = eo;
+          if (!(wv & bo)) { wv |= bo; s.expl++; }
+          if (!(wv & bn)) { wv |= bn; s.expl++; }
+          if (wv != eo) *ep_o = wv;
+        } else {
+          if (!(eo & bo)) { *ep_o = eo | bo; s.expl++; }
+          if (!(en & bn)) { *ep_n = en | bn; s.expl++; }
+        }
+        s.x = nx;                                                  // :199
+        s.y = ny;
+        dxv = dxm;
+        h = never ? rl.r_exploration : rl.r_revisit;               // :204-207
+      } else {
+        s.flags |= F_COLLIDED;                                     // :209
+        s.coll = s.coll < 65535 ? s.coll + 1 : 65535;              // :210
+        h = rl.r_invalid;                                          // :211
+      }
+    } else if (water) {
+      const int cd = w.code(0, s.y);
+      if (cd == THIRSTY) {                                         // fork plantos_env_new.py:237-240
+        const int pb = 2 * (s.y + R) - 64 * ((2 * w.yb) >> 6);
+        uint64_t* grow = st.grid + e * g.gstride + (int64_t)s.x * g.WPR + ((2 * w.yb) >> 6);
+        if (pb < 64) {
+          w.clo &= ~(1ull << (pb + 1));                            // 3 -> 2 (clear the high bit)
+          grow[0] = w.clo;
+        } else {
+          w.chi &= ~(1ull << (pb - 64 + 1));
+          grow[1] = w.chi;
+        }
+        w.refresh_centre();
+        h = rl.r_goal;
+      } else if (cd == HYD) {                                      // fork :241-242 (root raises)
+        h = rl.r_mistake;
+        if (!(s.flags & F_POISON_HYD)) atomicOr(st.err_bits, F_POISON_HYD);
+        s.flags |= F_POISON_HYD;
+      } else {
+        h = rl.r_water_empty;                                      // :221-222
+      }
+    }
+    double rew = rl.r_step;                                        // :164
+    rew += h;
+    const bool term = s.expl >= s.total;                           // :176, 244-246, 331
+    const bool trunc = s.step >= rl.max_steps;                     // :177
+    if (term && !(s.flags & F_BONUS)) {                            // :179-181
+      rew += rl.r_complete;
+      s.flags |= F_BONUS;
+    }
+    ret += rew;
+    a.reward[e] = (float)rew;
+    a.term[e] = term;
+    a.trunc[e] = trunc;
+    if ((term || trunc) && a.autoreset) {                          // DummyVecEnv auto-reset
+      if (a.tobs) {
+        obs_from_window<C, R, ONEWORD>(w, g.G, dxv, s.x, s.y, row, tpos, tvis);
+        float* t = a.tobs + e * g.D;
+        for (int k = 0; k < g.D; ++k) t[k] = row[k];
+      }
+      if (a.ep_ret_out) a.ep_ret_out[e] = ret;
+      if (a.ep_len_out) a.ep_len_out[e] = s.step;
+      s = reset_env(st, g, rl, e, s.episode);
+      st.ep_ret[e] = 0.0;
+      st.scal[e] = pack(s);
+      build_obs_generic(a, e, s.x, s.y, row, smem, tpos, tvis);  // fresh map: rare path
+    } else {
+      st.ep_ret[e] = ret;
+      st.scal[e] = pack(s);
+      obs_from_window<C, R, ONEWORD>(w, g.G, dxv, s.x, s.y, row, tpos, tvis);
+    }
+  }
+  __syncthreads();
+  const int64_t valid = a.n - e0 < kBlock ? a.n - e0 : kBlock;
+  store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.DS);
+}
+
 // reset(): masked device-rng reset, then obs of every env (obs may be NULL).
-template <int VC, int VR, bool ONEWORD>
 __global__ __launch_bounds__(kBlock) void pe_reset_kernel(StepArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* tdist = smem;
@@ -301,7 +391,7 @@ __global__ __launch_bounds__(kBlock) void pe_reset_kernel(StepArgs a) {
       a.st.ep_ret[e] = 0.0;
       a.st.scal[e] = pack(s);
     }
-    if (a.obs) build_obs<VC, VR, ONEWORD>(a, e, s.x, s.y, row, tdist, tpos, tvis);
+    if (a.obs) build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis);
   }
   if (!a.obs) return;
   __syncthreads();
@@ -555,10 +645,10 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
   dim3 grid((unsigned)((h->n + kBlock - 1) / kBlock)), block(kBlock);
   size_t lds = lds_bytes(h->g);
   switch (h->variant) {
-    case V_C16R6_1W: hipLaunchKernelGGL((pe_step_kernel<16, 6, true>), grid, block, lds, s, a); break;
-    case V_C16R6: hipLaunchKernelGGL((pe_step_kernel<16, 6, false>), grid, block, lds, s, a); break;
-    case V_C64R6: hipLaunchKernelGGL((pe_step_kernel<64, 6, false>), grid, block, lds, s, a); break;
-    default: hipLaunchKernelGGL((pe_step_kernel<0, 0, false>), grid, block, lds, s, a); break;
+    case V_C16R6_1W: hipLaunchKernelGGL((pe_step_fast<16, 6, true>), grid, block, lds, s, a); break;
+    case V_C16R6: hipLaunchKernelGGL((pe_step_fast<16, 6, false>), grid, block, lds, s, a); break;
+    case V_C64R6: hipLaunchKernelGGL((pe_step_fast<64, 6, false>), grid, block, lds, s, a); break;
+    default: hipLaunchKernelGGL(pe_step_kernel, grid, block, lds, s, a); break;
   }
   PE_HIP(hipGetLastError());
   return PE_OK;
@@ -567,12 +657,7 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
 int launch_reset(const pe_handle* h, const StepArgs& a, hipStream_t s) {
   dim3 grid((unsigned)((h->n + kBlock - 1) / kBlock)), block(kBlock);
   size_t lds = lds_bytes(h->g);
-  switch (h->variant) {
-    case V_C16R6_1W: hipLaunchKernelGGL((pe_reset_kernel<16, 6, true>), grid, block, lds, s, a); break;
-    case V_C16R6: hipLaunchKernelGGL((pe_reset_kernel<16, 6, false>), grid, block, lds, s, a); break;
-    case V_C64R6: hipLaunchKernelGGL((pe_reset_kernel<64, 6, false>), grid, block, lds, s, a); break;
-    default: hipLaunchKernelGGL((pe_reset_kernel<0, 0, false>), grid, block, lds, s, a); break;
-  }
+  hipLaunchKernelGGL(pe_reset_kernel, grid, block, lds, s, a);
   PE_HIP(hipGetLastError());
   return PE_OK;
 }
@@ -587,9 +672,9 @@ bool table_matches(const int8_t* dx, const int8_t* dy) {
 
 const char* variant_name(int v) {
   switch (v) {
-    case V_C16R6_1W: return "pe_step_kernel<C16,R6,1word>";
-    case V_C16R6: return "pe_step_kernel<C16,R6>";
-    case V_C64R6: return "pe_step_kernel<C64,R6>";
+    case V_C16R6_1W: return "pe_step_fast<C16,R6,1word>";
+    case V_C16R6: return "pe_step_fast<C16,R6>";
+    case V_C64R6: return "pe_step_fast<C64,R6>";
     default: return "pe_step_kernel<generic>";
   }
 }
