@@ -321,10 +321,10 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
         const int pb = 2 * (s.y + R) - 64 * ((2 * w.yb) >> 6);
         uint64_t* grow = st.grid + e * g.gstride + (int64_t)s.x * g.WPR + ((2 * w.yb) >> 6);
         if (pb < 64) {
-          w.clo &= ~(1ull << (pb + 1));                            // 3 -> 2 (clear the high bit)
+          w.clo &= ~(1ull << pb);                                  // code 3 -> 2: clear the low bit
           grow[0] = w.clo;
         } else {
-          w.chi &= ~(1ull << (pb - 64 + 1));
+          w.chi &= ~(1ull << (pb - 64));
           grow[1] = w.chi;
         }
         w.refresh_centre();
