@@ -73,6 +73,28 @@ def cpu_baseline(args, plants, obstacles):
                       f"oracle/plantos_oracle.c, OpenMP {threads} threads"}
 
 
+def measured_traffic(cfg):
+    """Per-launch HBM bytes of this kernel/config from the committed rocprofv3 PMC
+    summaries (profiles/pmc_*.json, tools/pmc_summary.py): FETCH_SIZE + WRITE_SIZE
+    in bytes, collected in separate passes.  PMC cannot run inside the timed
+    process, so the bench line cites the profile it took the number from."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json"))):
+        try:
+            d = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        c = d.get("config", {})
+        keys = ("envs_per_gpu", "grid", "rays", "lidar_range", "kernel")
+        if all(c.get(k) == cfg.get(k) for k in keys):
+            best = (p, d)
+    if best is None:
+        return None, None, None
+    p, d = best
+    return d["traffic"], d.get("traffic_hi"), os.path.relpath(p, REPO)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -160,6 +182,10 @@ def main():
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
                          "bytes_per_env_step": B, "kernel_ms": kern_ms},
         }
+        tr, tr_hi, src = measured_traffic(out["config"])
+        if tr is not None:
+            out["roofline"].update({"traffic": tr, "traffic_fetch_x2": tr_hi, "traffic_source": src,
+                                    "traffic_per_env_step": tr / n})
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, plants, obstacles)
         print(json.dumps(out), flush=True)

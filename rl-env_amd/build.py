@@ -11,7 +11,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "plantos_batch.hip")
-DEPS = [SRC, os.path.join(HERE, "csrc", "pe_device.hpp"), os.path.join(REPO, "include", "plantos_batch.h"),
+DEPS = [SRC, os.path.join(HERE, "csrc", "pe_device.hpp"), os.path.join(HERE, "csrc", "pe_fast.hpp"), os.path.join(REPO, "include", "plantos_batch.h"),
         os.path.join(HERE, "tools_gen_lidar.py")]
 OUT = os.path.join(HERE, "plantos_amd", "libplantos_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
