@@ -10,10 +10,15 @@
 //                                  plantos_env.py:271-274)
 //   vis    u32    [N][G][NW]       4-bit saturating visit counts min(v,15), padded by
 //                                  2 cells of value 10 on both sides (off-map reads
-//                                  1.0 = min(10,10)/10, plantos_env.py:307-311)
-//   v16    u16    [N][G*G]         exact visit counts (saturating at 65535), touched
-//                                  once per successful move (plantos_env.py:203)
-//   expl   u32    [N][EW]          explored bitmap (explored_map > 0)
+//                                  1.0 = min(10,10)/10, plantos_env.py:307-311).
+//                                  The nibble IS the visit count while it is < 15.
+//   v16    u16    [N][G*G]         exact visit count (saturating at 65535), valid only
+//                                  where the nibble is 15 (plantos_env.py:203); never
+//                                  cleared, never touched while a cell has < 15 visits
+//   expl   u32    [N][EW]          explored bitmap (explored_map > 0), authoritative
+//                                  only in F_EXPL_BITMAP mode; otherwise explored is
+//                                  derived: explored_map > 0  <=>  visit > 0 (true for
+//                                  every state the reference dynamics reach)
 //
 // Packed scalars (scal):
 //   w0 = x | y<<8 | step<<16        w1 = explored_count | total_cells<<16
@@ -33,6 +38,8 @@ enum : uint32_t {
   F_POISON_HYD = 4u,    // root env would raise TypeError (plantos_env.py:217-220)
   F_POISON_ACT = 8u,    // action < -4 (reference IndexError)
   F_NOROOM = 16u,       // last reset had no room (plantos_env.py:360-364)
+  F_EXPL_BITMAP = 32u,  // explored map decoupled from visits (injected state, e.g.
+                        // CurriculumWrapper visit_counts, A2C_training.py:88-93)
 };
 
 constexpr uint64_t kEven64 = 0x5555555555555555ull;  // low bit of every 2-bit code
@@ -196,6 +203,29 @@ __device__ __forceinline__ void vis_set(const State& st, const Geo& g, int64_t e
   *p = w;
 }
 
+__device__ __forceinline__ uint32_t nibble_get(const State& st, const Geo& g, int64_t e, int row, int col) {
+  int bit = 4 * (col + 2);
+  return (st.vis[e * g.vstride + (int64_t)row * g.NW + (bit >> 5)] >> (bit & 31)) & 15u;
+}
+
+// exact visit count of a real cell (nibble below 15, else the u16 overflow slot)
+__device__ __forceinline__ int visit_exact(const State& st, const Geo& g, int64_t e, int row, int col) {
+  const uint32_t n = nibble_get(st, g, e, row, col);
+  return n < 15u ? (int)n : (int)st.v16[e * g.hstride + row * g.G + col];
+}
+
+// visit_counts[cell] += 1 (plantos_env.py:203) given the cell's current nibble n;
+// the u16 slot is written only from the 15th visit on.
+__device__ __forceinline__ void visit_bump_exact(const State& st, const Geo& g, int64_t e, int cell, uint32_t n) {
+  uint16_t* vp = st.v16 + e * g.hstride + cell;
+  if (n == 14u) {
+    *vp = 15;
+  } else if (n == 15u) {
+    const uint32_t v = *vp;
+    *vp = (uint16_t)(v < 65535u ? v + 1u : 65535u);
+  }
+}
+
 __device__ __forceinline__ bool expl_test_set(const State& st, const Geo& g, int64_t e, int cell) {
   uint32_t* p = st.expl + e * g.estride + (cell >> 5);
   uint32_t m = 1u << (cell & 31);
@@ -238,9 +268,8 @@ __device__ inline Scal reset_env(const State& st, const Geo& g, const Rules& rl,
     for (int w = 0; w < g.WPR; ++w) st.grid[e * g.gstride + (int64_t)row * g.WPR + w] = st.tab->grid_pad[w];
     for (int w = 0; w < g.NW; ++w) st.vis[e * g.vstride + (int64_t)row * g.NW + w] = st.tab->vis_pad[w];
   }
-  uint32_t* v32 = reinterpret_cast<uint32_t*>(st.v16 + e * g.hstride);
-  for (int k = 0; k < (int)(g.hstride / 2); ++k) v32[k] = 0u;
-  for (int k = 0; k < g.estride; ++k) st.expl[e * g.estride + k] = 0u;
+  // v16 and the explored bitmap are not cleared: every nibble is now 0 (v16 is
+  // read only behind a nibble of 15) and a fresh episode is in derived-explored mode.
 
   Stream rng;
   rng.init(rl.seed, rl.env_off + (uint32_t)e, episode);
@@ -279,7 +308,7 @@ __device__ inline Scal reset_env(const State& st, const Geo& g, const Rules& rl,
     return s;
   }
   // random.sample(list(available), P): set-based selection, row-major list
-  uint16_t* picks = st.v16 + e * g.hstride;  // scratch: pick order (cleared below)
+  uint16_t* picks = st.v16 + e * g.hstride;  // scratch: pick order (v16 is dead here)
   for (int i = 0; i < rl.P; ++i) {
     int c;
     for (;;) {
@@ -295,15 +324,12 @@ __device__ inline Scal reset_env(const State& st, const Geo& g, const Rules& rl,
     int c = picks[i];
     if (rng.random53() < rl.p_thirsty) grid_set(st, g, e, c / G, c % G + g.R, THIRSTY);
   }
-  for (int i = 0; i < rl.P; ++i) picks[i] = 0;
   // rover: choice(list(available - plants)), plantos_env.py:370-372
   int rc = nth_cell(st, g, e, (int)rng.below((uint32_t)(nfree - rl.P)), 1);
   s.x = rc / G;
   s.y = rc % G;
-  st.v16[e * g.hstride + rc] = 1;  // plantos_env.py:146-147
-  vis_set(st, g, e, s.x, s.y, 1u);
-  expl_test_set(st, g, e, rc);     // plantos_env.py:236
-  return s;
+  vis_set(st, g, e, s.x, s.y, 1u);  // visit[rover] = 1 (plantos_env.py:146-147); explored[rover]
+  return s;                         // = 2 follows from it (plantos_env.py:236)
 }
 
 }  // namespace pe

@@ -1,0 +1,109 @@
+// pe_quad.hpp -- the quadrant-split fused step kernel (compile-time C, R).
+//
+// One workgroup = 4 waves = 64 envs; lane l of every wave works on env e0+l, and
+// wave w owns LIDAR rays [w*C/4, (w+1)*C/4) -- one compass quadrant -- so the
+// per-wave ray code is fully unrolled with compile-time offsets and the wave
+// index is the only branch (wave-uniform: no divergence).  This gives 4 waves
+// per SIMD at the headline batch instead of 1 (one lane per env), so the load
+// latency of one workgroup hides behind the ray-march and obs stores of others.
+//
+//   round 1  every wave: packed scalars + action of its 64 envs (same addresses
+//            in all 4 waves: one fetch, L1 hits after)
+//   round 2  the 2R+3 grid rows and 7 visit rows around the rover are split over
+//            the waves (row k loaded by wave k%4) and parked in LDS, [row][env];
+//            wave 0 also fetches what the state commit needs (raw target visit
+//            word, u16 overflow slot, explored words in bitmap mode, raw centre
+//            grid words for watering)
+//   barrier
+//   every wave re-derives the transition from LDS (cheap, identical), wave 0
+//   commits the state; each wave ray-marches its quadrant over the post-move
+//   window read from LDS at a per-lane row offset, and writes its slice of the
+//   obs row into the LDS obs tile
+//   barrier (+ auto-reset slow path in wave 0 if any env of the block is done)
+//   the 256 threads stream the [64 x D] obs tile to HBM with 16-B stores.
+#pragma once
+#include "pe_device.hpp"
+
+namespace pe {
+
+constexpr int kQuadWaves = 4;
+constexpr int kQuadEnvs = 64;
+
+// compile-time extent of the dx offsets of rays [i0, i1)
+template <int C, int R>
+constexpr int ray_dx_min(int i0, int i1) {
+  int m = 0;
+  for (int i = i0; i < i1; ++i)
+    for (int r = 0; r < R; ++r) m = LidarTab<C, R>::dx[i][r] < m ? LidarTab<C, R>::dx[i][r] : m;
+  return m;
+}
+template <int C, int R>
+constexpr int ray_dx_max(int i0, int i1) {
+  int m = 0;
+  for (int i = i0; i < i1; ++i)
+    for (int r = 0; r < R; ++r) m = LidarTab<C, R>::dx[i][r] > m ? LidarTab<C, R>::dx[i][r] : m;
+  return m;
+}
+
+// Grid row xr as a 64-bit window of padded 2-bit codes starting at padded column
+// yb (w0 = word, o = bit offset of yb); off-map rows read as obstacles.
+template <bool ONEWORD>
+__device__ __forceinline__ uint64_t quad_row(const uint64_t* gb, const Geo& g, int xr, int w0, int o) {
+  if (xr < 0 || xr >= g.G) return kEven64;
+  if constexpr (ONEWORD) {
+    return gb[xr];
+  } else {
+    const uint64_t* p = gb + (int64_t)xr * g.WPR + w0;
+    const uint64_t lo = p[0];
+    const uint64_t hi = (w0 + 1 < g.WPR) ? p[1] : 0ull;
+    return o ? ((lo >> o) | (hi << (64 - o))) : lo;
+  }
+}
+
+// Rays [W*C/4, (W+1)*C/4) of one env: first hit over the post-move window rows
+// read from LDS (row k of the [row][env] block = grid row x-R-1+k), written as
+// obs[5i .. 5i+4] (plantos_env.py:260-292).
+template <int C, int R, int W>
+__device__ __forceinline__ void quad_rays(const uint64_t* lrow, int lane, int kc, int sh, bool watered, float* row) {
+  constexpr int I0 = W * C / kQuadWaves, I1 = (W + 1) * C / kQuadWaves;
+  constexpr int LO = ray_dx_min<C, R>(I0, I1), HI = ray_dx_max<C, R>(I0, I1);
+  uint64_t win[HI - LO + 1];
+#pragma unroll
+  for (int j = 0; j <= HI - LO; ++j) win[j] = lrow[(kc + LO + j) * kQuadEnvs + lane] >> sh;
+  if constexpr (LO <= 0 && HI >= 0) {
+    // watering turned the rover's cell thirsty -> hydrated (code 3 -> 2)
+    if (watered) win[-LO] &= ~(1ull << (2 * R));
+  }
+  using T = LidarTab<C, R>;
+#pragma unroll
+  for (int i = I0; i < I1; ++i) {
+    float dist = 1.0f;  // nothing hit: float(R / R), plantos_env.py:262
+    int ent = EMPTY;
+#pragma unroll
+    for (int r = R; r >= 1; --r) {
+      const int dx = T::dx[i][r - 1], dy = T::dy[i][r - 1];
+      const int cd = (int)((win[dx - LO] >> (2 * (dy + R))) & 3u);
+      if (cd != EMPTY) {
+        dist = (float)((double)r / (double)R);  // float(r / R), plantos_env.py:288
+        ent = cd;
+      }
+    }
+    row[5 * i] = dist;
+    row[5 * i + 1] = ent == 0 ? 1.0f : 0.0f;
+    row[5 * i + 2] = ent == 1 ? 1.0f : 0.0f;
+    row[5 * i + 3] = ent == 2 ? 1.0f : 0.0f;
+    row[5 * i + 4] = ent == 3 ? 1.0f : 0.0f;
+  }
+}
+
+// One row lx of the 5x5 visit slice (plantos_env.py:298-313) from the LDS visit
+// rows (row k = visit row x-3+k, 8 nibbles from padded column ybv).
+__device__ __forceinline__ void quad_slice_row(const uint32_t* lvis, int lane, int lx, int dxv, int vs, bool bump,
+                                               uint32_t nib, int C, float* row, const float* tvis) {
+  uint32_t v = lvis[(dxv + 1 + lx) * kQuadEnvs + lane] >> vs;
+  if (lx == 2 && bump) v = (v & ~0xF00u) | (nib << 8);  // the move's own visit (:203)
+#pragma unroll
+  for (int ly = 0; ly < 5; ++ly) row[5 * C + 2 + 5 * lx + ly] = tvis[(v >> (4 * ly)) & 15u];
+}
+
+}  // namespace pe

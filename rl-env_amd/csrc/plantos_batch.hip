@@ -10,6 +10,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -18,6 +19,7 @@
 #include "lidar_tables.inc"
 #include "pe_device.hpp"
 #include "pe_fast.hpp"
+#include "pe_quad.hpp"
 
 using namespace pe;
 
@@ -101,14 +103,16 @@ __device__ __forceinline__ double transition(const StepArgs& a, int64_t e, Scal&
       if (ok) ok = grid_code(a.st, g, e, nx, ny + g.R) != OBST;
       if (ok) {
         const int cell = nx * g.G + ny;
-        uint16_t* vp = a.st.v16 + e * g.hstride + cell;
-        const uint32_t v = *vp;
-        const bool never = v == 0;                              // :197
-        const uint32_t v1 = v < 65535u ? v + 1u : 65535u;       // :203
-        *vp = (uint16_t)v1;
-        vis_set(a.st, g, e, nx, ny, v1 < 15u ? v1 : 15u);
-        if (expl_test_set(a.st, g, e, s.x * g.G + s.y)) s.expl++;  // explored[old] = 1, :198
-        if (expl_test_set(a.st, g, e, cell)) s.expl++;             // explored[new] = 2, :200
+        const uint32_t n = nibble_get(a.st, g, e, nx, ny);
+        const bool never = n == 0u;                             // :197
+        vis_set(a.st, g, e, nx, ny, n < 15u ? n + 1u : 15u);    // :203
+        visit_bump_exact(a.st, g, e, cell, n);
+        if (s.flags & F_EXPL_BITMAP) {
+          if (expl_test_set(a.st, g, e, s.x * g.G + s.y)) s.expl++;  // explored[old] = 1, :198
+          if (expl_test_set(a.st, g, e, cell)) s.expl++;             // explored[new] = 2, :200
+        } else if (never) {
+          s.expl++;  // derived mode: explored[old] is set, explored[new] was 0 iff never visited
+        }
         s.x = nx;                                                  // :199
         s.y = ny;
         h = never ? rl.r_exploration : rl.r_revisit;               // :204-207
@@ -267,21 +271,25 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
     uint16_t* vp = st.v16 + e * g.hstride + (inb ? cell_n : 0);
     uint32_t* ep_o = st.expl + e * g.estride + (cell_o >> 5);
     uint32_t* ep_n = st.expl + e * g.estride + ((inb ? cell_n : cell_o) >> 5);
+    const bool bitmap = (s.flags & F_EXPL_BITMAP) != 0u;
     uint32_t v = 0u, eo = 0u, en = 0u;
     if (inb) {
       v = *vp;
-      eo = *ep_o;
-      en = *ep_n;
+      if (bitmap) {
+        eo = *ep_o;
+        en = *ep_n;
+      }
     }
     double h = 0.0;
     int dxv = 0;
     if (mv) {
       const bool ok = inb && w.code(dxm, ny) != OBST;              // :193-195
       if (ok) {
-        const bool never = v == 0u;                                // :197
-        const uint32_t v1 = v < 65535u ? v + 1u : 65535u;          // :203
-        *vp = (uint16_t)v1;
-        const uint32_t nib = v1 < 15u ? v1 : 15u;
+        const uint32_t n = (sel3<uint32_t>(dxm, w.vis32(2), w.vis32(3), w.vis32(4)) >> (4 * (ny + 2 - w.ybv))) & 15u;
+        const bool never = n == 0u;                                // :197
+        const uint32_t nib = n < 15u ? n + 1u : 15u;               // :203
+        if (n == 14u) *vp = 15;
+        else if (n == 15u) *vp = (uint16_t)(v < 65535u ? v + 1u : 65535u);
         const int pb = 4 * (ny + 2) - 32 * ((4 * w.ybv) >> 5);
         uint32_t* vrow = st.vis + e * g.vstride + (int64_t)nx * g.NW + ((4 * w.ybv) >> 5);
 #pragma unroll
@@ -296,15 +304,19 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
             }
           }
         }
-        const uint32_t bo = 1u << (cell_o & 31), bn = 1u << (cell_n & 31);
-        if ((cell_o >> 5) == (cell_n >> 5)) {                      // explored[old]=1, [new]=2 (:198-200)
-          uint32_t wv = eo;
-          if (!(wv & bo)) { wv |= bo; s.expl++; }
-          if (!(wv & bn)) { wv |= bn; s.expl++; }
-          if (wv != eo) *ep_o = wv;
-        } else {
-          if (!(eo & bo)) { *ep_o = eo | bo; s.expl++; }
-          if (!(en & bn)) { *ep_n = en | bn; s.expl++; }
+        if (bitmap) {
+          const uint32_t bo = 1u << (cell_o & 31), bn = 1u << (cell_n & 31);
+          if ((cell_o >> 5) == (cell_n >> 5)) {                    // explored[old]=1, [new]=2 (:198-200)
+            uint32_t wv = eo;
+            if (!(wv & bo)) { wv |= bo; s.expl++; }
+            if (!(wv & bn)) { wv |= bn; s.expl++; }
+            if (wv != eo) *ep_o = wv;
+          } else {
+            if (!(eo & bo)) { *ep_o = eo | bo; s.expl++; }
+            if (!(en & bn)) { *ep_n = en | bn; s.expl++; }
+          }
+        } else if (never) {
+          s.expl++;                                                // derived explored mode
         }
         s.x = nx;                                                  // :199
         s.y = ny;
@@ -372,6 +384,247 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
   store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.DS);
 }
 
+// Quadrant-split fused step (pe_quad.hpp): 4 waves x 64 envs per workgroup.
+// Same semantics as pe_step_kernel + transition().
+template <int R>
+constexpr int quad_tile_off() {
+  return (kTabFloats + (2 * R + 3) * kQuadEnvs * 2 + 7 * kQuadEnvs + 3) & ~3;
+}
+
+template <int C, int R, bool ONEWORD>
+__global__ __launch_bounds__(256) void pe_step_quad(StepArgs a) {
+  constexpr int NR = 2 * R + 3, NV = 7, EPB = kQuadEnvs;
+  static_assert(ONEWORD || R <= 14, "funnel-shifted window row must hold 2R+5 cells");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* tdist = smem;
+  float* tpos = smem + 72;
+  float* tvis = smem + 328;
+  uint64_t* lrow = reinterpret_cast<uint64_t*>(smem + kTabFloats);  // [NR][EPB]
+  uint32_t* lvis = reinterpret_cast<uint32_t*>(lrow + NR * EPB);    // [NV][EPB]
+  float* rows = smem + quad_tile_off<R>();                          // [EPB][D]
+  const Geo& g = a.g;
+  const Rules& rl = a.rl;
+  const State& st = a.st;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t e0 = (int64_t)blockIdx.x * EPB;
+  const int64_t e = e0 + lane;
+  const bool live = e < a.n;
+
+  // ---- round 1: env-indexed loads (all waves)
+  uint4 sw = make_uint4(0u, 0u, 0u, 0u);
+  int64_t action = 0;
+  double ret = 0.0;
+  if (live) {
+    sw = st.scal[e];
+    action = a.act_bytes == 8 ? reinterpret_cast<const int64_t*>(a.actions)[e]
+                              : (int64_t)reinterpret_cast<const int32_t*>(a.actions)[e];
+    if (wv == 0) ret = st.ep_ret[e];
+  }
+  load_tables(smem, st.tab);
+  Scal s = unpack(sw);
+  bool mv = false, water = false, bad = false;
+  int dxm = 0, dym = 0;
+  if (action < 4) {                                              // plantos_env.py:166
+    const int64_t ai = action < 0 ? action + 4 : action;         // Python negative index
+    if (ai < 0) {
+      bad = true;                                                // reference IndexError
+    } else {
+      mv = true;                                                 // :186 N,E,S,W
+      dxm = ai == 0 ? -1 : (ai == 2 ? 1 : 0);
+      dym = ai == 1 ? 1 : (ai == 3 ? -1 : 0);
+    }
+  } else {
+    water = true;
+  }
+  const int nx = s.x + dxm, ny = s.y + dym;
+  const bool inb = mv && nx >= 0 && nx < g.G && ny >= 0 && ny < g.G;  // :193-195
+  const int nyc = inb ? ny : s.y;
+  const int yb = ONEWORD ? 0 : (s.y > 0 ? s.y - 1 : 0);
+  const int ybv = s.y > 0 ? s.y - 1 : 0;
+  const uint64_t* gb = st.grid + e * g.gstride;
+  const int cell_o = s.x * g.G + s.y, cell_n = nx * g.G + nyc;
+  const int pbw = (4 * (nyc + 2)) >> 5;  // word of the target's visit nibble
+
+  // ---- round 2: this wave's share of the window rows -> LDS
+  uint32_t vraw = 0u, v16v = 0u, eo = 0u, en = 0u;
+  uint64_t craw = 0ull;
+  if (live) {
+    const int w0 = (2 * yb) >> 6, o = (2 * yb) & 63;
+#pragma unroll
+    for (int j = 0; j < (NR + 3) / 4; ++j) {
+      const int k = wv + 4 * j;
+      if (k < NR) lrow[k * EPB + lane] = quad_row<ONEWORD>(gb, g, s.x - R - 1 + k, w0, o);
+    }
+    const int vw = (4 * ybv) >> 5, vo = (4 * ybv) & 31;
+    const uint32_t* vb = st.vis + e * g.vstride + vw;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = wv + 4 * j;
+      if (k < NV) {
+        const int xr = s.x - 3 + k;
+        uint32_t lo = 0xAAAAAAAAu, hi = 0xAAAAAAAAu;  // off-map row: visit 10 (reads 1.0)
+        if (xr >= 0 && xr < g.G) {
+          lo = vb[(int64_t)xr * g.NW];
+          hi = vb[(int64_t)xr * g.NW + 1];
+        }
+        lvis[k * EPB + lane] = vo ? ((lo >> vo) | (hi << (32 - vo))) : lo;
+      }
+    }
+    if (wv == 0) {  // what the state commit needs
+      if (inb) {
+        vraw = st.vis[e * g.vstride + (int64_t)nx * g.NW + pbw];
+        v16v = st.v16[e * g.hstride + cell_n];
+        if (s.flags & F_EXPL_BITMAP) {
+          eo = st.expl[e * g.estride + (cell_o >> 5)];
+          en = st.expl[e * g.estride + (cell_n >> 5)];
+        }
+      }
+      if (!ONEWORD && water) craw = gb[(int64_t)s.x * g.WPR + ((2 * (s.y + R)) >> 6)];
+    }
+  }
+  __syncthreads();
+
+  // ---- transition from LDS (every wave; wave 0 commits)
+  s.step = s.step < 65535 ? s.step + 1 : 65535;                  // :162
+  bool ok = false, watered = false, wet_hyd = false;
+  uint32_t n = 0u;
+  int dxv = 0;
+  double h = 0.0;
+  if (mv) {
+    const uint64_t rt = lrow[(R + 1 + dxm) * EPB + lane];
+    ok = inb && ((rt >> (2 * (nyc + R - yb))) & 3u) != OBST;      // :193-195 (plants walkable)
+    if (ok) {
+      n = (lvis[(3 + dxm) * EPB + lane] >> (4 * (nyc + 2 - ybv))) & 15u;
+      h = n == 0u ? rl.r_exploration : rl.r_revisit;              // :197, 204-207
+      dxv = dxm;
+    } else {
+      s.flags |= F_COLLIDED;                                      // :209
+      s.coll = s.coll < 65535 ? s.coll + 1 : 65535;               // :210
+      h = rl.r_invalid;                                           // :211
+    }
+  } else if (water) {
+    const uint64_t rc = lrow[(R + 1) * EPB + lane];
+    const int cd = (int)((rc >> (2 * (s.y + R - yb))) & 3u);
+    if (cd == THIRSTY) {                                          // fork plantos_env_new.py:237-240
+      watered = true;
+      h = rl.r_goal;
+    } else if (cd == HYD) {                                       // fork :241-242 (root raises)
+      wet_hyd = true;
+      h = rl.r_mistake;
+    } else {
+      h = rl.r_water_empty;                                       // :221-222
+    }
+  }
+  const int xp = s.x + dxv, yp = ok ? ny : s.y;
+  const uint32_t nib = n < 15u ? n + 1u : 15u;                    // :203
+  float* row = rows + lane * g.D;
+  bool done = false;
+  if (live) {
+    const int kc = dxv + R + 1;
+    const int sh = 2 * (yp - yb);
+    const int vs = 4 * (yp - ybv);
+    switch (wv) {
+      case 0:
+        quad_rays<C, R, 0>(lrow, lane, kc, sh, watered, row);
+        quad_slice_row(lvis, lane, 0, dxv, vs, ok, nib, C, row, tvis);
+        quad_slice_row(lvis, lane, 4, dxv, vs, ok, nib, C, row, tvis);
+        break;
+      case 1:
+        quad_rays<C, R, 1>(lrow, lane, kc, sh, watered, row);
+        quad_slice_row(lvis, lane, 1, dxv, vs, ok, nib, C, row, tvis);
+        row[5 * C] = tpos[xp];                                    // :294-296
+        row[5 * C + 1] = tpos[yp];
+        break;
+      case 2:
+        quad_rays<C, R, 2>(lrow, lane, kc, sh, watered, row);
+        quad_slice_row(lvis, lane, 2, dxv, vs, ok, nib, C, row, tvis);
+        break;
+      default:
+        quad_rays<C, R, 3>(lrow, lane, kc, sh, watered, row);
+        quad_slice_row(lvis, lane, 3, dxv, vs, ok, nib, C, row, tvis);
+        break;
+    }
+    if (wv == 0) {
+      // ---- commit (plantos_env.py:160-222)
+      if (ok) {
+        const int pb = (4 * (ny + 2)) & 31;
+        st.vis[e * g.vstride + (int64_t)nx * g.NW + pbw] = (vraw & ~(0xFu << pb)) | (nib << pb);
+        uint16_t* vp = st.v16 + e * g.hstride + cell_n;
+        if (n == 14u) *vp = 15;
+        else if (n == 15u) *vp = (uint16_t)(v16v < 65535u ? v16v + 1u : 65535u);
+        if (s.flags & F_EXPL_BITMAP) {                            // explored[old]=1, [new]=2 (:198-200)
+          const uint32_t bo = 1u << (cell_o & 31), bn = 1u << (cell_n & 31);
+          uint32_t* ep_o = st.expl + e * g.estride + (cell_o >> 5);
+          uint32_t* ep_n = st.expl + e * g.estride + (cell_n >> 5);
+          if ((cell_o >> 5) == (cell_n >> 5)) {
+            uint32_t w = eo;
+            if (!(w & bo)) { w |= bo; s.expl++; }
+            if (!(w & bn)) { w |= bn; s.expl++; }
+            if (w != eo) *ep_o = w;
+          } else {
+            if (!(eo & bo)) { *ep_o = eo | bo; s.expl++; }
+            if (!(en & bn)) { *ep_n = en | bn; s.expl++; }
+          }
+        } else if (n == 0u) {
+          s.expl++;  // derived mode: explored[new] was 0 iff never visited
+        }
+      }
+      if (watered) {
+        const int bit = 2 * (s.y + R);
+        if constexpr (ONEWORD) {
+          const_cast<uint64_t*>(gb)[s.x] = lrow[(R + 1) * EPB + lane] & ~(1ull << bit);  // code 3 -> 2
+        } else {
+          const_cast<uint64_t*>(gb)[(int64_t)s.x * g.WPR + (bit >> 6)] = craw & ~(1ull << (bit & 63));
+        }
+      }
+      if (bad) {
+        s.flags |= F_POISON_ACT;
+        atomicOr(st.err_bits, F_POISON_ACT);
+      }
+      if (wet_hyd && !(s.flags & F_POISON_HYD)) {
+        s.flags |= F_POISON_HYD;
+        atomicOr(st.err_bits, F_POISON_HYD);
+      }
+      s.x = xp;                                                   // :199
+      s.y = yp;
+      double rew = rl.r_step;                                     // :164
+      rew += h;
+      const bool term = s.expl >= s.total;                        // :176, 244-246, 331
+      const bool trunc = s.step >= rl.max_steps;                  // :177
+      if (term && !(s.flags & F_BONUS)) {                         // :179-181
+        rew += rl.r_complete;
+        s.flags |= F_BONUS;
+      }
+      ret += rew;
+      a.reward[e] = (float)rew;
+      a.term[e] = term;
+      a.trunc[e] = trunc;
+      st.ep_ret[e] = ret;
+      st.scal[e] = pack(s);
+      done = (term || trunc) && a.autoreset;
+    }
+  }
+  // ---- DummyVecEnv auto-reset (rare): wave 0, after the whole obs row is in LDS
+  if (__syncthreads_or(done)) {
+    if (done) {
+      if (a.tobs) {
+        float* t = a.tobs + e * g.D;
+        for (int k = 0; k < g.D; ++k) t[k] = row[k];
+      }
+      if (a.ep_ret_out) a.ep_ret_out[e] = ret;
+      if (a.ep_len_out) a.ep_len_out[e] = s.step;
+      s = reset_env(st, g, rl, e, s.episode);
+      st.ep_ret[e] = 0.0;
+      st.scal[e] = pack(s);
+      build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis);
+    }
+    __syncthreads();
+  }
+  const int64_t valid = a.n - e0 < EPB ? a.n - e0 : EPB;
+  store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D);
+}
+
 // reset(): masked device-rng reset, then obs of every env (obs may be NULL).
 __global__ __launch_bounds__(kBlock) void pe_reset_kernel(StepArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -424,9 +677,6 @@ __global__ __launch_bounds__(kBlock) void pe_load_maps_kernel(StepArgs a, int k,
       if (code) grid_set(a.st, g, e, row, col + g.R, code);
     }
   }
-  uint32_t* v32 = reinterpret_cast<uint32_t*>(a.st.v16 + e * g.hstride);
-  for (int q = 0; q < (int)(g.hstride / 2); ++q) v32[q] = 0u;
-  for (int q = 0; q < g.estride; ++q) a.st.expl[e * g.estride + q] = 0u;
   Scal s = unpack(a.st.scal[e]);
   s.x = rover[2 * j];
   s.y = rover[2 * j + 1];
@@ -436,10 +686,7 @@ __global__ __launch_bounds__(kBlock) void pe_load_maps_kernel(StepArgs a, int k,
   s.episode += 1u;
   s.total = g.GG - n_obst;
   s.expl = 1;
-  const int rc = s.x * g.G + s.y;
-  a.st.v16[e * g.hstride + rc] = 1;
-  vis_set(a.st, g, e, s.x, s.y, 1u);
-  expl_test_set(a.st, g, e, rc);
+  vis_set(a.st, g, e, s.x, s.y, 1u);  // plantos_env.py:146-147 (explored derived, :236)
   a.st.scal[e] = pack(s);
   a.st.ep_ret[e] = 0.0;
   float* row = rows + threadIdx.x * g.DS;
@@ -485,14 +732,17 @@ __global__ void pe_get_cells_kernel(StepArgs a, uint8_t* cells, int32_t* visits,
   const int c = (int)(t - e * g.GG);
   const int row = c / g.G, col = c - row * g.G;
   if (cells) cells[t] = (uint8_t)grid_code(a.st, g, e, row, col + g.R);
-  if (visits) visits[t] = a.st.v16[e * g.hstride + c];
+  if (visits) visits[t] = visit_exact(a.st, g, e, row, col);
   if (explored) {
-    uint32_t w = a.st.expl[e * g.estride + (c >> 5)];
-    int8_t v = (w >> (c & 31)) & 1u ? 1 : 0;
-    if (v) {
-      Scal s = unpack(a.st.scal[e]);
-      if (s.x == row && s.y == col) v = 2;
+    Scal s = unpack(a.st.scal[e]);
+    int8_t v;
+    if (s.flags & F_EXPL_BITMAP) {
+      uint32_t w = a.st.expl[e * g.estride + (c >> 5)];
+      v = (w >> (c & 31)) & 1u ? 1 : 0;
+    } else {
+      v = nibble_get(a.st, g, e, row, col) ? 1 : 0;  // explored_map > 0 <=> visit > 0
     }
+    if (v && s.x == row && s.y == col) v = 2;  // plantos_env.py:200, 236
     explored[t] = v;
   }
 }
@@ -512,36 +762,43 @@ __global__ void pe_get_scal_kernel(StepArgs a, int32_t* scal) {
   o[PE_S_EPISODE] = (int32_t)s.episode;
 }
 
-// set_state (cells/visits): one thread per (env, row) rebuilds the packed rows.
-__global__ void pe_set_rows_kernel(StepArgs a, const uint8_t* cells, const int32_t* visits) {
-  const Geo& g = a.g;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (int64_t)a.n * g.G) return;
-  const int64_t e = t / g.G;
-  const int row = (int)(t - e * g.G);
-  if (cells) {
-    for (int w = 0; w < g.WPR; ++w) a.st.grid[e * g.gstride + (int64_t)row * g.WPR + w] = a.st.tab->grid_pad[w];
-    for (int col = 0; col < g.G; ++col) {
-      int code = cells[e * g.GG + row * g.G + col] & 3;
-      if (code) grid_set(a.st, g, e, row, col + g.R, code);
-    }
-  }
-  if (visits) {
-    for (int w = 0; w < g.NW; ++w) a.st.vis[e * g.vstride + (int64_t)row * g.NW + w] = a.st.tab->vis_pad[w];
-    for (int col = 0; col < g.G; ++col) {
-      int32_t v = visits[e * g.GG + row * g.G + col];
-      uint32_t vc = v <= 0 ? 0u : (v >= 65535 ? 65535u : (uint32_t)v);
-      a.st.v16[e * g.hstride + row * g.G + col] = (uint16_t)vc;
-      vis_set(a.st, g, e, row, col, vc < 15u ? vc : 15u);
-    }
-  }
-}
-
-// set_state (explored bitmap + scalars + derived counters): one thread per env.
-__global__ void pe_set_env_kernel(StepArgs a, const int8_t* explored, const int32_t* scal) {
+// set_state: one thread per env, in this order: (1) if explored stays derived but
+// visits change, freeze the current explored map into the bitmap; (2) cells,
+// (3) visits, (4) explored, (5) scalars; (6) derived counters and the explored
+// mode: derived (bitmap not read) iff explored_map > 0 <=> visit > 0 everywhere.
+__global__ void pe_set_env_kernel(StepArgs a, const uint8_t* cells, const int32_t* visits, const int8_t* explored,
+                                  const int32_t* scal) {
   const Geo& g = a.g;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= a.n) return;
+  Scal s = unpack(a.st.scal[e]);
+  uint32_t* eb = a.st.expl + e * g.estride;
+  if (!(s.flags & F_EXPL_BITMAP) && visits && !explored) {
+    for (int w = 0; w < g.estride; ++w) eb[w] = 0u;
+    for (int c = 0; c < g.GG; ++c)
+      if (nibble_get(a.st, g, e, c / g.G, c % g.G)) eb[c >> 5] |= 1u << (c & 31);
+    s.flags |= F_EXPL_BITMAP;
+  }
+  if (cells) {
+    for (int row = 0; row < g.G; ++row) {
+      for (int w = 0; w < g.WPR; ++w) a.st.grid[e * g.gstride + (int64_t)row * g.WPR + w] = a.st.tab->grid_pad[w];
+      for (int col = 0; col < g.G; ++col) {
+        int code = cells[e * g.GG + row * g.G + col] & 3;
+        if (code) grid_set(a.st, g, e, row, col + g.R, code);
+      }
+    }
+  }
+  if (visits) {
+    for (int row = 0; row < g.G; ++row) {
+      for (int w = 0; w < g.NW; ++w) a.st.vis[e * g.vstride + (int64_t)row * g.NW + w] = a.st.tab->vis_pad[w];
+      for (int col = 0; col < g.G; ++col) {
+        int32_t v = visits[e * g.GG + row * g.G + col];
+        uint32_t vc = v <= 0 ? 0u : (v >= 65535 ? 65535u : (uint32_t)v);
+        a.st.v16[e * g.hstride + row * g.G + col] = (uint16_t)vc;
+        vis_set(a.st, g, e, row, col, vc < 15u ? vc : 15u);
+      }
+    }
+  }
   if (explored) {
     for (int w = 0; w < g.estride; ++w) {
       uint32_t bits = 0;
@@ -549,22 +806,32 @@ __global__ void pe_set_env_kernel(StepArgs a, const int8_t* explored, const int3
         int c = w * 32 + b;
         if (c < g.GG && explored[e * g.GG + c] > 0) bits |= 1u << b;
       }
-      a.st.expl[e * g.estride + w] = bits;
+      eb[w] = bits;
     }
+    s.flags |= F_EXPL_BITMAP;
   }
-  Scal s = unpack(a.st.scal[e]);
   if (scal) {
     const int32_t* i = scal + e * PE_NSCAL;
     s.x = i[PE_S_X];
     s.y = i[PE_S_Y];
     s.step = i[PE_S_STEP] < 0 ? 0 : (i[PE_S_STEP] > 65535 ? 65535 : i[PE_S_STEP]);
     s.coll = i[PE_S_COLL] < 0 ? 0 : (i[PE_S_COLL] > 65535 ? 65535 : i[PE_S_COLL]);
-    s.flags = (i[PE_S_COLLIDED] ? F_COLLIDED : 0u) | (i[PE_S_BONUS] ? F_BONUS : 0u) |
+    s.flags = (s.flags & F_EXPL_BITMAP) | (i[PE_S_COLLIDED] ? F_COLLIDED : 0u) | (i[PE_S_BONUS] ? F_BONUS : 0u) |
               ((uint32_t)(i[PE_S_POISONED] & 7) << 2);
     s.episode = (uint32_t)i[PE_S_EPISODE];
   }
   int ex = 0, ob = 0;
-  for (int w = 0; w < g.estride; ++w) ex += __popc(a.st.expl[e * g.estride + w]);
+  if (s.flags & F_EXPL_BITMAP) {
+    bool same = true;
+    for (int c = 0; c < g.GG; ++c) {
+      const bool bit = (eb[c >> 5] >> (c & 31)) & 1u;
+      ex += bit;
+      same = same && (bit == (nibble_get(a.st, g, e, c / g.G, c % g.G) != 0u));
+    }
+    if (same) s.flags &= ~F_EXPL_BITMAP;
+  } else {
+    for (int c = 0; c < g.GG; ++c) ex += nibble_get(a.st, g, e, c / g.G, c % g.G) != 0u;
+  }
   for (int row = 0; row < g.G; ++row)
     for (int w = 0; w < g.WPR; ++w) {
       uint64_t v = a.st.grid[e * g.gstride + (int64_t)row * g.WPR + w];
@@ -639,16 +906,39 @@ StepArgs base_args(const pe_handle* h) {
 
 size_t lds_bytes(const Geo& g) { return sizeof(float) * (size_t)(kTabFloats + kBlock * g.DS); }
 
-enum Variant { V_GENERIC = 0, V_C16R6_1W = 1, V_C16R6 = 2, V_C64R6 = 3 };
+// Step kernel variants.  The quadrant kernels (4 waves x 64 envs per workgroup)
+// are the default for the specialized geometries; the one-lane-per-env kernels
+// stay selectable (PE_STEP_KERNEL=lane) for A/B measurement.
+enum Variant {
+  V_GENERIC = 0, V_C16R6_1W = 1, V_C16R6 = 2, V_C64R6 = 3,
+  V_QUAD_C16R6_1W = 4, V_QUAD_C16R6 = 5, V_QUAD_C64R6 = 6
+};
+
+size_t quad_lds_bytes(const Geo& g) {
+  return sizeof(float) * ((size_t)((kTabFloats + (2 * g.R + 3) * kQuadEnvs * 2 + 7 * kQuadEnvs + 3) & ~3) +
+                          (size_t)kQuadEnvs * g.D);
+}
+
+bool is_quad(int v) { return v >= V_QUAD_C16R6_1W; }
 
 int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
-  dim3 grid((unsigned)((h->n + kBlock - 1) / kBlock)), block(kBlock);
-  size_t lds = lds_bytes(h->g);
-  switch (h->variant) {
-    case V_C16R6_1W: hipLaunchKernelGGL((pe_step_fast<16, 6, true>), grid, block, lds, s, a); break;
-    case V_C16R6: hipLaunchKernelGGL((pe_step_fast<16, 6, false>), grid, block, lds, s, a); break;
-    case V_C64R6: hipLaunchKernelGGL((pe_step_fast<64, 6, false>), grid, block, lds, s, a); break;
-    default: hipLaunchKernelGGL(pe_step_kernel, grid, block, lds, s, a); break;
+  if (is_quad(h->variant)) {
+    dim3 grid((unsigned)((h->n + kQuadEnvs - 1) / kQuadEnvs)), block(kQuadWaves * 64);
+    size_t lds = quad_lds_bytes(h->g);
+    switch (h->variant) {
+      case V_QUAD_C16R6_1W: hipLaunchKernelGGL((pe_step_quad<16, 6, true>), grid, block, lds, s, a); break;
+      case V_QUAD_C16R6: hipLaunchKernelGGL((pe_step_quad<16, 6, false>), grid, block, lds, s, a); break;
+      default: hipLaunchKernelGGL((pe_step_quad<64, 6, false>), grid, block, lds, s, a); break;
+    }
+  } else {
+    dim3 grid((unsigned)((h->n + kBlock - 1) / kBlock)), block(kBlock);
+    size_t lds = lds_bytes(h->g);
+    switch (h->variant) {
+      case V_C16R6_1W: hipLaunchKernelGGL((pe_step_fast<16, 6, true>), grid, block, lds, s, a); break;
+      case V_C16R6: hipLaunchKernelGGL((pe_step_fast<16, 6, false>), grid, block, lds, s, a); break;
+      case V_C64R6: hipLaunchKernelGGL((pe_step_fast<64, 6, false>), grid, block, lds, s, a); break;
+      default: hipLaunchKernelGGL(pe_step_kernel, grid, block, lds, s, a); break;
+    }
   }
   PE_HIP(hipGetLastError());
   return PE_OK;
@@ -675,6 +965,9 @@ const char* variant_name(int v) {
     case V_C16R6_1W: return "pe_step_fast<C16,R6,1word>";
     case V_C16R6: return "pe_step_fast<C16,R6>";
     case V_C64R6: return "pe_step_fast<C64,R6>";
+    case V_QUAD_C16R6_1W: return "pe_step_quad<C16,R6,1word>";
+    case V_QUAD_C16R6: return "pe_step_quad<C16,R6>";
+    case V_QUAD_C64R6: return "pe_step_quad<C64,R6>";
     default: return "pe_step_kernel<generic>";
   }
 }
@@ -804,6 +1097,10 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   h->variant = V_GENERIC;
   if (C == 16 && R == 6 && table_matches<16, 6>(ldx, ldy)) h->variant = g.WPR == 1 ? V_C16R6_1W : V_C16R6;
   if (C == 64 && R == 6 && table_matches<64, 6>(ldx, ldy)) h->variant = V_C64R6;
+  const char* kenv = std::getenv("PE_STEP_KERNEL");  // "lane": one-lane-per-env kernels (A/B)
+  const bool lane_kernels = kenv && std::strcmp(kenv, "lane") == 0;
+  if (!lane_kernels && h->variant != V_GENERIC) h->variant += V_QUAD_C16R6_1W - V_C16R6_1W;
+  if (is_quad(h->variant) && quad_lds_bytes(g) > 160 * 1024) h->variant -= V_QUAD_C16R6_1W - V_C16R6_1W;
   h->kname = variant_name(h->variant);
 
   // one device allocation carved into 256-B aligned arrays
@@ -959,12 +1256,7 @@ int pe_set_state(pe_handle* h, const uint8_t* cells, const int32_t* visits, cons
   if (rc) return rc;
   StepArgs a = base_args(h);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (cells || visits) {
-    int64_t total = (int64_t)h->n * h->g.G;
-    hipLaunchKernelGGL(pe_set_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a, cells, visits);
-    PE_HIP(hipGetLastError());
-  }
-  hipLaunchKernelGGL(pe_set_env_kernel, dim3((h->n + 255) / 256), dim3(256), 0, s, a, explored, scalars);
+  hipLaunchKernelGGL(pe_set_env_kernel, dim3((h->n + 127) / 128), dim3(128), 0, s, a, cells, visits, explored, scalars);
   PE_HIP(hipGetLastError());
   return PE_OK;
 }
