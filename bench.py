@@ -50,6 +50,9 @@ def parse():
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--action-steps", type=int, default=64, help="distinct pre-generated action rows")
     p.add_argument("--gather", action="store_true", help="RCCL gather of (obs,reward,done) to rank 0 each step")
+    p.add_argument("--graph", type=int, default=64,
+                   help="capture this many consecutive steps in one hipGraph and replay it (0: one host "
+                        "launch per step); every captured step is a full pe_step launch")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     return p.parse_args()
@@ -132,15 +135,31 @@ def main():
     for t in range(args.warmup):
         one_step(t)
     torch.cuda.synchronize()
+    K = args.steps
+    # graph mode: one graph = `chunk` consecutive pe_step launches; step k of a replay
+    # reads action row k % T (plain mode: step t reads row t % T).  K = reps * chunk + rest.
+    chunk = min(args.graph, K) if (args.graph > 1 and not args.gather) else 0
+    graph = None
+    if chunk > 1:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for k in range(chunk):
+                b.step(actions[k % T])
+        torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    K = args.steps
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record()
-    for k in range(K):
-        one_step(args.warmup + k)
+    if graph is not None:
+        for k in range(K // chunk):
+            graph.replay()
+        for k in range(K % chunk):
+            one_step(k)
+    else:
+        for k in range(K):
+            one_step(args.warmup + k)
     ev1.record()
     torch.cuda.synchronize()
     if dist:
@@ -177,7 +196,9 @@ def main():
                                    f"{obstacles} obstacles, auto-reset, actions in HBM",
                        "envs_per_gpu": n, "grid": G, "rays": C, "lidar_range": R,
                        "parallelism": f"env-shard x{world}" + (" + rccl gather" if args.gather else ""),
-                       "kernel": b.kernel_name},
+                       "kernel": b.kernel_name,
+                       "launch": f"hipGraph replay, {chunk} pe_step launches per graph" if graph is not None
+                       else "one host launch per step"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
                          "bytes_per_env_step": B, "kernel_ms": kern_ms},

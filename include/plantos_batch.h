@@ -129,7 +129,7 @@ int pe_get_info(pe_handle* h, int32_t* info, void* stream);
 /* Canonical state, reference terms: cells u8[n,G,G] (pe_cell), visits i32[n,G,G],
  * explored i8[n,G,G] (0/1/2), scalars i32[n,PE_NSCAL].  Any pointer may be NULL
  * (get: skipped; set: that part is left unchanged).  set recomputes derived
- * counters (explored/total cells) from the arrays. Visits saturate at 65535. */
+ * counters (explored/total cells) from the arrays. Visits are exact int32 counts. */
 int pe_get_state(pe_handle* h, uint8_t* cells, int32_t* visits, int8_t* explored, int32_t* scalars,
                  void* stream);
 int pe_set_state(pe_handle* h, const uint8_t* cells, const int32_t* visits, const int8_t* explored,

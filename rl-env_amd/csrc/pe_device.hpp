@@ -12,9 +12,10 @@
 //                                  2 cells of value 10 on both sides (off-map reads
 //                                  1.0 = min(10,10)/10, plantos_env.py:307-311).
 //                                  The nibble IS the visit count while it is < 15.
-//   v16    u16    [N][G*G]         exact visit count (saturating at 65535), valid only
-//                                  where the nibble is 15 (plantos_env.py:203); never
-//                                  cleared, never touched while a cell has < 15 visits
+//   vx     u32    [N][G*G]         exact visit count, valid only where the nibble is 15
+//                                  (plantos_env.py:203): written once at the 15th
+//                                  visit, then bumped by no-return atomics (never read
+//                                  by the step kernels); never cleared
 //   expl   u32    [N][EW]          explored bitmap (explored_map > 0), authoritative
 //                                  only in F_EXPL_BITMAP mode; otherwise explored is
 //                                  derived: explored_map > 0  <=>  visit > 0 (true for
@@ -69,7 +70,7 @@ struct State {
   double* ep_ret;
   uint64_t* grid;
   uint32_t* vis;
-  uint16_t* v16;
+  uint32_t* vx;    // visit-count overflow slots (see layout above)
   uint32_t* expl;
   const Tables* tab;
   const signed char* ldx;  // [C][R] LIDAR offsets (generic kernel)
@@ -211,18 +212,17 @@ __device__ __forceinline__ uint32_t nibble_get(const State& st, const Geo& g, in
 // exact visit count of a real cell (nibble below 15, else the u16 overflow slot)
 __device__ __forceinline__ int visit_exact(const State& st, const Geo& g, int64_t e, int row, int col) {
   const uint32_t n = nibble_get(st, g, e, row, col);
-  return n < 15u ? (int)n : (int)st.v16[e * g.hstride + row * g.G + col];
+  return n < 15u ? (int)n : (int)st.vx[e * g.hstride + row * g.G + col];
 }
 
-// visit_counts[cell] += 1 (plantos_env.py:203) given the cell's current nibble n;
-// the u16 slot is written only from the 15th visit on.
+// visit_counts[cell] += 1 (plantos_env.py:203) given the cell's current nibble n:
+// the overflow slot is set at the 15th visit and bumped in memory after that.
 __device__ __forceinline__ void visit_bump_exact(const State& st, const Geo& g, int64_t e, int cell, uint32_t n) {
-  uint16_t* vp = st.v16 + e * g.hstride + cell;
+  uint32_t* vp = st.vx + e * g.hstride + cell;
   if (n == 14u) {
-    *vp = 15;
+    *vp = 15u;
   } else if (n == 15u) {
-    const uint32_t v = *vp;
-    *vp = (uint16_t)(v < 65535u ? v + 1u : 65535u);
+    atomicAdd(vp, 1u);  // no-return atomic: the count is never read by a step
   }
 }
 
@@ -268,7 +268,7 @@ __device__ inline Scal reset_env(const State& st, const Geo& g, const Rules& rl,
     for (int w = 0; w < g.WPR; ++w) st.grid[e * g.gstride + (int64_t)row * g.WPR + w] = st.tab->grid_pad[w];
     for (int w = 0; w < g.NW; ++w) st.vis[e * g.vstride + (int64_t)row * g.NW + w] = st.tab->vis_pad[w];
   }
-  // v16 and the explored bitmap are not cleared: every nibble is now 0 (v16 is
+  // vx and the explored bitmap are not cleared: every nibble is now 0 (vx is
   // read only behind a nibble of 15) and a fresh episode is in derived-explored mode.
 
   Stream rng;
@@ -308,7 +308,7 @@ __device__ inline Scal reset_env(const State& st, const Geo& g, const Rules& rl,
     return s;
   }
   // random.sample(list(available), P): set-based selection, row-major list
-  uint16_t* picks = st.v16 + e * g.hstride;  // scratch: pick order (v16 is dead here)
+  uint32_t* picks = st.vx + e * g.hstride;  // scratch: pick order (all nibbles are 0 here)
   for (int i = 0; i < rl.P; ++i) {
     int c;
     for (;;) {
@@ -317,7 +317,7 @@ __device__ inline Scal reset_env(const State& st, const Geo& g, const Rules& rl,
       if (grid_code(st, g, e, c / G, c % G + g.R) == EMPTY) break;  // else already selected
     }
     grid_set(st, g, e, c / G, c % G + g.R, HYD);
-    picks[i] = (uint16_t)c;
+    picks[i] = (uint32_t)c;
   }
   // thirsty draws in sample order, plantos_env.py:367-369
   for (int i = 0; i < rl.P; ++i) {

@@ -1,33 +1,32 @@
 // pe_quad.hpp -- the quadrant-split fused step kernel (compile-time C, R).
 //
-// One workgroup = 4 waves = 64 envs; lane l of every wave works on env e0+l, and
-// wave w owns LIDAR rays [w*C/4, (w+1)*C/4) -- one compass quadrant -- so the
-// per-wave ray code is fully unrolled with compile-time offsets and the wave
-// index is the only branch (wave-uniform: no divergence).  This gives 4 waves
-// per SIMD at the headline batch instead of 1 (one lane per env), so the load
-// latency of one workgroup hides behind the ray-march and obs stores of others.
+// One workgroup = NW waves (4 or 8) = 64 envs; lane l of every wave works on env
+// e0+l, and wave w owns LIDAR rays [w*C/NW, (w+1)*C/NW) -- one compass sector --
+// so the per-wave ray code is fully unrolled with compile-time offsets and the
+// wave index is the only branch (wave-uniform: no divergence).  At NW=8 this is
+// 8 waves per SIMD at the headline batch instead of 1 (one lane per env), so the
+// load latency of one workgroup hides behind the work of the others.
 //
 //   round 1  every wave: packed scalars + action of its 64 envs (same addresses
 //            in all 4 waves: one fetch, L1 hits after)
 //   round 2  the 2R+3 grid rows and 7 visit rows around the rover are split over
-//            the waves (row k loaded by wave k%4) and parked in LDS, [row][env];
-//            wave 0 also fetches what the state commit needs (raw target visit
-//            word, u16 overflow slot, explored words in bitmap mode, raw centre
-//            grid words for watering)
+//            the waves (row k loaded by wave k%NW) and parked in LDS, [row][env];
+//            the commit wave (NW-1) also fetches what the state commit needs (raw
+//            target visit word, u16 overflow slot, explored words in bitmap mode,
+//            raw centre grid word for watering)
 //   barrier
-//   every wave re-derives the transition from LDS (cheap, identical), wave 0
-//   commits the state; each wave ray-marches its quadrant over the post-move
+//   every wave re-derives the transition from LDS (cheap, identical), wave NW-1
+//   commits the state; each wave ray-marches its sector over the post-move
 //   window read from LDS at a per-lane row offset, and writes its slice of the
 //   obs row into the LDS obs tile
-//   barrier (+ auto-reset slow path in wave 0 if any env of the block is done)
-//   the 256 threads stream the [64 x D] obs tile to HBM with 16-B stores.
+//   barrier (+ auto-reset slow path in the commit wave if any env is done)
+//   the 64*NW threads stream the [64 x D] obs tile to HBM with 16-B stores.
 #pragma once
 #include "pe_device.hpp"
 
 namespace pe {
 
-constexpr int kQuadWaves = 4;
-constexpr int kQuadEnvs = 64;
+constexpr int kQuadEnvs = 64;  // envs per workgroup (one per lane of every wave)
 
 // compile-time extent of the dx offsets of rays [i0, i1)
 template <int C, int R>
@@ -60,12 +59,12 @@ __device__ __forceinline__ uint64_t quad_row(const uint64_t* gb, const Geo& g, i
   }
 }
 
-// Rays [W*C/4, (W+1)*C/4) of one env: first hit over the post-move window rows
-// read from LDS (row k of the [row][env] block = grid row x-R-1+k), written as
-// obs[5i .. 5i+4] (plantos_env.py:260-292).
-template <int C, int R, int W>
+// Rays [W*C/NW, (W+1)*C/NW) of one env (the sector of wave W): first hit over the
+// post-move window rows read from LDS (row k of the [row][env] block = grid row
+// x-R-1+k), written as obs[5i .. 5i+4] (plantos_env.py:260-292).
+template <int C, int R, int NW, int W>
 __device__ __forceinline__ void quad_rays(const uint64_t* lrow, int lane, int kc, int sh, bool watered, float* row) {
-  constexpr int I0 = W * C / kQuadWaves, I1 = (W + 1) * C / kQuadWaves;
+  constexpr int I0 = W * C / NW, I1 = (W + 1) * C / NW;
   constexpr int LO = ray_dx_min<C, R>(I0, I1), HI = ray_dx_max<C, R>(I0, I1);
   uint64_t win[HI - LO + 1];
 #pragma unroll
@@ -93,6 +92,18 @@ __device__ __forceinline__ void quad_rays(const uint64_t* lrow, int lane, int kc
     row[5 * i + 2] = ent == 1 ? 1.0f : 0.0f;
     row[5 * i + 3] = ent == 2 ? 1.0f : 0.0f;
     row[5 * i + 4] = ent == 3 ? 1.0f : 0.0f;
+  }
+}
+
+// Wave-uniform dispatch of the sector code (wv comes from readfirstlane).
+template <int C, int R, int NW, int W = 0>
+__device__ __forceinline__ void sector_rays(int wv, const uint64_t* lrow, int lane, int kc, int sh, bool watered,
+                                            float* row) {
+  if constexpr (W < NW) {
+    if (wv == W)
+      quad_rays<C, R, NW, W>(lrow, lane, kc, sh, watered, row);
+    else
+      sector_rays<C, R, NW, W + 1>(wv, lrow, lane, kc, sh, watered, row);
   }
 }
 

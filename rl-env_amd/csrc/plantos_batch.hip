@@ -268,13 +268,11 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
     Window<R, ONEWORD> w;
     w.load(st, g, e, s.x, s.y);
     const int cell_o = s.x * g.G + s.y, cell_n = nx * g.G + ny;
-    uint16_t* vp = st.v16 + e * g.hstride + (inb ? cell_n : 0);
     uint32_t* ep_o = st.expl + e * g.estride + (cell_o >> 5);
     uint32_t* ep_n = st.expl + e * g.estride + ((inb ? cell_n : cell_o) >> 5);
     const bool bitmap = (s.flags & F_EXPL_BITMAP) != 0u;
-    uint32_t v = 0u, eo = 0u, en = 0u;
+    uint32_t eo = 0u, en = 0u;
     if (inb) {
-      v = *vp;
       if (bitmap) {
         eo = *ep_o;
         en = *ep_n;
@@ -288,8 +286,7 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
         const uint32_t n = (sel3<uint32_t>(dxm, w.vis32(2), w.vis32(3), w.vis32(4)) >> (4 * (ny + 2 - w.ybv))) & 15u;
         const bool never = n == 0u;                                // :197
         const uint32_t nib = n < 15u ? n + 1u : 15u;               // :203
-        if (n == 14u) *vp = 15;
-        else if (n == 15u) *vp = (uint16_t)(v < 65535u ? v + 1u : 65535u);
+        visit_bump_exact(st, g, e, cell_n, n);
         const int pb = 4 * (ny + 2) - 32 * ((4 * w.ybv) >> 5);
         uint32_t* vrow = st.vis + e * g.vstride + (int64_t)nx * g.NW + ((4 * w.ybv) >> 5);
 #pragma unroll
@@ -384,6 +381,35 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
   store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.DS);
 }
 
+// Diagnostic phase ablation (tools/ablate.py builds a SEPARATE library with
+// -DPE_ABLATE=bits; the product library is built without it): 1 = no obs tile
+// store, 2 = no ray-march, 4 = no round-2 window loads, 8 = no state commit.
+#ifdef PE_ABLATE
+constexpr int kAblate = PE_ABLATE;
+#else
+constexpr int kAblate = 0;
+#endif
+
+// Diagnostic phase stamps (tools/stamps.py builds a SEPARATE library with
+// -DPE_STAMPS): lane 0 of every wave of the sector kernel records s_memrealtime
+// (100 MHz) at 8 points; pe_debug_stamps() copies them out.  Not in the product build.
+#ifdef PE_STAMPS
+__device__ uint64_t g_stamps[16384 * 8];
+#define PE_STAMP(k)                                                                         \
+  do {                                                                                      \
+    uint64_t _t;                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");        \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    const int _w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);                     \
+    if ((threadIdx.x & 63) == 0 && _w < 16384) g_stamps[_w * 8 + (k)] = _t;                \
+  } while (0)
+#else
+#define PE_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
 // Quadrant-split fused step (pe_quad.hpp): 4 waves x 64 envs per workgroup.
 // Same semantics as pe_step_kernel + transition().
 template <int R>
@@ -391,9 +417,10 @@ constexpr int quad_tile_off() {
   return (kTabFloats + (2 * R + 3) * kQuadEnvs * 2 + 7 * kQuadEnvs + 3) & ~3;
 }
 
-template <int C, int R, bool ONEWORD>
-__global__ __launch_bounds__(256) void pe_step_quad(StepArgs a) {
-  constexpr int NR = 2 * R + 3, NV = 7, EPB = kQuadEnvs;
+template <int C, int R, bool ONEWORD, int NW>
+__global__ __launch_bounds__(64 * NW) void pe_step_quad(StepArgs a) {
+  constexpr int NR = 2 * R + 3, NV = 7, EPB = kQuadEnvs, CW = NW - 1;  // CW: commit wave
+  static_assert(C % NW == 0, "rays must split evenly over the waves");
   static_assert(ONEWORD || R <= 14, "funnel-shifted window row must hold 2R+5 cells");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* tdist = smem;
@@ -411,18 +438,30 @@ __global__ __launch_bounds__(256) void pe_step_quad(StepArgs a) {
   const int64_t e = e0 + lane;
   const bool live = e < a.n;
 
-  // ---- round 1: env-indexed loads (all waves)
-  uint4 sw = make_uint4(0u, 0u, 0u, 0u);
+  // ---- round 1: env-indexed loads (all waves).  Every thread also plays a LOADER
+  // role for round 2: LT = NW threads per env (env le, part sub), so each load
+  // instruction reads LT consecutive rows of 64/LT envs instead of one row of 64.
+  PE_STAMP(0);
+  constexpr int LT = NW;
+  const int le = threadIdx.x / LT, sub = threadIdx.x % LT;
+  const int64_t el = e0 + le;
+  const bool llive = el < a.n;
+  uint4 sw = make_uint4(0u, 0u, 0u, 0u), lw = make_uint4(0u, 0u, 0u, 0u);
   int64_t action = 0;
   double ret = 0.0;
   if (live) {
     sw = st.scal[e];
     action = a.act_bytes == 8 ? reinterpret_cast<const int64_t*>(a.actions)[e]
                               : (int64_t)reinterpret_cast<const int32_t*>(a.actions)[e];
-    if (wv == 0) ret = st.ep_ret[e];
+    if (wv == CW) ret = st.ep_ret[e];
   }
+  if (llive) lw = st.scal[el];
   load_tables(smem, st.tab);
   Scal s = unpack(sw);
+#ifdef PE_STAMPS
+  if ((int)(s.x + lw.x) == -12345) g_stamps[0] = 1;  // consume round 1 before the stamp
+#endif
+  PE_STAMP(1);
   bool mv = false, water = false, bad = false;
   int dxm = 0, dym = 0;
   if (action < 4) {                                              // plantos_env.py:166
@@ -446,44 +485,95 @@ __global__ __launch_bounds__(256) void pe_step_quad(StepArgs a) {
   const int cell_o = s.x * g.G + s.y, cell_n = nx * g.G + nyc;
   const int pbw = (4 * (nyc + 2)) >> 5;  // word of the target's visit nibble
 
-  // ---- round 2: this wave's share of the window rows -> LDS
-  uint32_t vraw = 0u, v16v = 0u, eo = 0u, en = 0u;
+  // ---- round 2: window rows of env le -> LDS [row][env] (loader role)
+  uint32_t vraw = 0u, eo = 0u, en = 0u;
   uint64_t craw = 0ull;
-  if (live) {
-    const int w0 = (2 * yb) >> 6, o = (2 * yb) & 63;
+  if (llive && !(kAblate & 4)) {
+    const int lx = (int)(lw.x & 0xFF), ly = (int)((lw.x >> 8) & 0xFF);
+    const uint64_t* lgb = st.grid + el * g.gstride;
+    const int base = lx - R - 1;  // grid row of LDS row 0
+    if constexpr (ONEWORD) {
+      // row pairs (16 B, aligned: env blocks are 16-B aligned, pairs start on even rows)
+      const int ps = base & ~1;
+      constexpr int NP = (NR + 2) / 2;
 #pragma unroll
-    for (int j = 0; j < (NR + 3) / 4; ++j) {
-      const int k = wv + 4 * j;
-      if (k < NR) lrow[k * EPB + lane] = quad_row<ONEWORD>(gb, g, s.x - R - 1 + k, w0, o);
-    }
-    const int vw = (4 * ybv) >> 5, vo = (4 * ybv) & 31;
-    const uint32_t* vb = st.vis + e * g.vstride + vw;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int k = wv + 4 * j;
-      if (k < NV) {
-        const int xr = s.x - 3 + k;
-        uint32_t lo = 0xAAAAAAAAu, hi = 0xAAAAAAAAu;  // off-map row: visit 10 (reads 1.0)
-        if (xr >= 0 && xr < g.G) {
-          lo = vb[(int64_t)xr * g.NW];
-          hi = vb[(int64_t)xr * g.NW + 1];
-        }
-        lvis[k * EPB + lane] = vo ? ((lo >> vo) | (hi << (32 - vo))) : lo;
-      }
-    }
-    if (wv == 0) {  // what the state commit needs
-      if (inb) {
-        vraw = st.vis[e * g.vstride + (int64_t)nx * g.NW + pbw];
-        v16v = st.v16[e * g.hstride + cell_n];
-        if (s.flags & F_EXPL_BITMAP) {
-          eo = st.expl[e * g.estride + (cell_o >> 5)];
-          en = st.expl[e * g.estride + (cell_n >> 5)];
+      for (int j = 0; j < (NP + LT - 1) / LT; ++j) {
+        const int pp = sub + LT * j;
+        if (pp < NP) {
+          const int ra = ps + 2 * pp;
+          uint64_t va = kEven64, vb2 = kEven64;  // off-map rows: obstacles
+          if (ra >= 0 && ra + 1 < g.G) {
+            const uint4 q = *reinterpret_cast<const uint4*>(lgb + ra);
+            va = (uint64_t)q.x | ((uint64_t)q.y << 32);
+            vb2 = (uint64_t)q.z | ((uint64_t)q.w << 32);
+          } else {
+            if (ra >= 0 && ra < g.G) va = lgb[ra];
+            if (ra + 1 >= 0 && ra + 1 < g.G) vb2 = lgb[ra + 1];
+          }
+          const int ka = ra - base;
+          if (ka >= 0 && ka < NR) lrow[ka * EPB + le] = va;
+          if (ka + 1 >= 0 && ka + 1 < NR) lrow[(ka + 1) * EPB + le] = vb2;
         }
       }
-      if (!ONEWORD && water) craw = gb[(int64_t)s.x * g.WPR + ((2 * (s.y + R)) >> 6)];
+      // visit rows: one 16-B row per load (g.NW == 4), funnel-shifted to ybv
+      const int lybv = ly > 0 ? ly - 1 : 0;
+      const int vw = (4 * lybv) >> 5, vo = (4 * lybv) & 31;
+#pragma unroll
+      for (int j = 0; j < (NV + LT - 1) / LT; ++j) {
+        const int k = sub + LT * j;
+        if (k < NV) {
+          const int xr = lx - 3 + k;
+          uint32_t lo = 0xAAAAAAAAu, hi = 0xAAAAAAAAu;  // off-map row: visit 10 (reads 1.0)
+          if (xr >= 0 && xr < g.G) {
+            const uint4 q = *reinterpret_cast<const uint4*>(st.vis + el * g.vstride + (int64_t)xr * 4);
+            lo = vw == 0 ? q.x : (vw == 1 ? q.y : q.z);
+            hi = vw == 0 ? q.y : (vw == 1 ? q.z : q.w);
+          }
+          lvis[k * EPB + le] = vo ? ((lo >> vo) | (hi << (32 - vo))) : lo;
+        }
+      }
+    } else {
+      const int lyb = ly > 0 ? ly - 1 : 0;
+      const int w0 = (2 * lyb) >> 6, o = (2 * lyb) & 63;
+#pragma unroll
+      for (int j = 0; j < (NR + LT - 1) / LT; ++j) {
+        const int k = sub + LT * j;
+        if (k < NR) lrow[k * EPB + le] = quad_row<false>(lgb, g, base + k, w0, o);
+      }
+      const int lybv = ly > 0 ? ly - 1 : 0;
+      const int vw = (4 * lybv) >> 5, vo = (4 * lybv) & 31;
+      const uint32_t* vb = st.vis + el * g.vstride + vw;
+#pragma unroll
+      for (int j = 0; j < (NV + LT - 1) / LT; ++j) {
+        const int k = sub + LT * j;
+        if (k < NV) {
+          const int xr = lx - 3 + k;
+          uint32_t lo = 0xAAAAAAAAu, hi = 0xAAAAAAAAu;
+          if (xr >= 0 && xr < g.G) {
+            lo = vb[(int64_t)xr * g.NW];
+            hi = vb[(int64_t)xr * g.NW + 1];
+          }
+          lvis[k * EPB + le] = vo ? ((lo >> vo) | (hi << (32 - vo))) : lo;
+        }
+      }
     }
   }
+  if (live && wv == CW) {  // what the state commit needs (lane = env)
+    if (inb) {
+      vraw = st.vis[e * g.vstride + (int64_t)nx * g.NW + pbw];
+      if (s.flags & F_EXPL_BITMAP) {
+        eo = st.expl[e * g.estride + (cell_o >> 5)];
+        en = st.expl[e * g.estride + (cell_n >> 5)];
+      }
+    }
+    if (!ONEWORD && water) craw = gb[(int64_t)s.x * g.WPR + ((2 * (s.y + R)) >> 6)];
+  }
+#ifdef PE_STAMPS
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
+  PE_STAMP(2);
   __syncthreads();
+  PE_STAMP(3);
 
   // ---- transition from LDS (every wave; wave 0 commits)
   s.step = s.step < 65535 ? s.step + 1 : 65535;                  // :162
@@ -524,35 +614,18 @@ __global__ __launch_bounds__(256) void pe_step_quad(StepArgs a) {
     const int kc = dxv + R + 1;
     const int sh = 2 * (yp - yb);
     const int vs = 4 * (yp - ybv);
-    switch (wv) {
-      case 0:
-        quad_rays<C, R, 0>(lrow, lane, kc, sh, watered, row);
-        quad_slice_row(lvis, lane, 0, dxv, vs, ok, nib, C, row, tvis);
-        quad_slice_row(lvis, lane, 4, dxv, vs, ok, nib, C, row, tvis);
-        break;
-      case 1:
-        quad_rays<C, R, 1>(lrow, lane, kc, sh, watered, row);
-        quad_slice_row(lvis, lane, 1, dxv, vs, ok, nib, C, row, tvis);
-        row[5 * C] = tpos[xp];                                    // :294-296
-        row[5 * C + 1] = tpos[yp];
-        break;
-      case 2:
-        quad_rays<C, R, 2>(lrow, lane, kc, sh, watered, row);
-        quad_slice_row(lvis, lane, 2, dxv, vs, ok, nib, C, row, tvis);
-        break;
-      default:
-        quad_rays<C, R, 3>(lrow, lane, kc, sh, watered, row);
-        quad_slice_row(lvis, lane, 3, dxv, vs, ok, nib, C, row, tvis);
-        break;
+    if constexpr (!(kAblate & 2)) sector_rays<C, R, NW>(wv, lrow, lane, kc, sh, watered, row);
+    for (int lx = wv; lx < 5; lx += NW) quad_slice_row(lvis, lane, lx, dxv, vs, ok, nib, C, row, tvis);
+    if (wv == (NW == 4 ? 1 : 5)) {
+      row[5 * C] = tpos[xp];                                      // :294-296
+      row[5 * C + 1] = tpos[yp];
     }
-    if (wv == 0) {
+    if (wv == CW && !(kAblate & 8)) {
       // ---- commit (plantos_env.py:160-222)
       if (ok) {
         const int pb = (4 * (ny + 2)) & 31;
         st.vis[e * g.vstride + (int64_t)nx * g.NW + pbw] = (vraw & ~(0xFu << pb)) | (nib << pb);
-        uint16_t* vp = st.v16 + e * g.hstride + cell_n;
-        if (n == 14u) *vp = 15;
-        else if (n == 15u) *vp = (uint16_t)(v16v < 65535u ? v16v + 1u : 65535u);
+        visit_bump_exact(st, g, e, cell_n, n);
         if (s.flags & F_EXPL_BITMAP) {                            // explored[old]=1, [new]=2 (:198-200)
           const uint32_t bo = 1u << (cell_o & 31), bn = 1u << (cell_n & 31);
           uint32_t* ep_o = st.expl + e * g.estride + (cell_o >> 5);
@@ -605,8 +678,11 @@ __global__ __launch_bounds__(256) void pe_step_quad(StepArgs a) {
       done = (term || trunc) && a.autoreset;
     }
   }
-  // ---- DummyVecEnv auto-reset (rare): wave 0, after the whole obs row is in LDS
-  if (__syncthreads_or(done)) {
+  PE_STAMP(4);
+  // ---- DummyVecEnv auto-reset (rare): commit wave, after the whole obs row is in LDS
+  const int any_done = __syncthreads_or(done);
+  PE_STAMP(5);
+  if (any_done) {
     if (done) {
       if (a.tobs) {
         float* t = a.tobs + e * g.D;
@@ -622,7 +698,12 @@ __global__ __launch_bounds__(256) void pe_step_quad(StepArgs a) {
     __syncthreads();
   }
   const int64_t valid = a.n - e0 < EPB ? a.n - e0 : EPB;
-  store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D);
+  if constexpr (!(kAblate & 1)) store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D);
+  PE_STAMP(6);
+#ifdef PE_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  PE_STAMP(7);
 }
 
 // reset(): masked device-rng reset, then obs of every env (obs may be NULL).
@@ -793,8 +874,8 @@ __global__ void pe_set_env_kernel(StepArgs a, const uint8_t* cells, const int32_
       for (int w = 0; w < g.NW; ++w) a.st.vis[e * g.vstride + (int64_t)row * g.NW + w] = a.st.tab->vis_pad[w];
       for (int col = 0; col < g.G; ++col) {
         int32_t v = visits[e * g.GG + row * g.G + col];
-        uint32_t vc = v <= 0 ? 0u : (v >= 65535 ? 65535u : (uint32_t)v);
-        a.st.v16[e * g.hstride + row * g.G + col] = (uint16_t)vc;
+        uint32_t vc = v <= 0 ? 0u : (uint32_t)v;
+        a.st.vx[e * g.hstride + row * g.G + col] = vc;
         vis_set(a.st, g, e, row, col, vc < 15u ? vc : 15u);
       }
     }
@@ -863,6 +944,8 @@ struct pe_handle {
   size_t bytes;
   int variant;
   const char* kname;
+  size_t lds_floor;  // PE_LDS_FLOOR (diagnostics): minimum dynamic LDS per step workgroup
+  int quad_waves;    // waves per workgroup of the sector kernel (4 or 8; PE_QUAD_WAVES)
 };
 
 namespace {
@@ -886,12 +969,29 @@ int hip_fail(hipError_t e, const char* what) {
 
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
-int bind_device(const pe_handle* h) {
-  int cur = -1;
-  PE_HIP(hipGetDevice(&cur));
-  if (cur != h->device) PE_HIP(hipSetDevice(h->device));
-  return PE_OK;
-}
+// Binds the handle's device for one API call and restores the caller's device
+// afterwards (the library never leaves the calling thread on another device).
+struct DeviceGuard {
+  int prev = -1;
+  int rc = PE_OK;
+  explicit DeviceGuard(const pe_handle* h) {
+    hipError_t e = hipGetDevice(&prev);
+    if (e != hipSuccess) {
+      rc = hip_fail(e, "hipGetDevice");
+      prev = -1;
+      return;
+    }
+    if (prev != h->device) {
+      e = hipSetDevice(h->device);
+      if (e != hipSuccess) rc = hip_fail(e, "hipSetDevice");
+    } else {
+      prev = -1;
+    }
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
 
 StepArgs base_args(const pe_handle* h) {
   StepArgs a;
@@ -923,13 +1023,21 @@ bool is_quad(int v) { return v >= V_QUAD_C16R6_1W; }
 
 int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
   if (is_quad(h->variant)) {
-    dim3 grid((unsigned)((h->n + kQuadEnvs - 1) / kQuadEnvs)), block(kQuadWaves * 64);
+    const int nw = h->quad_waves;
+    dim3 grid((unsigned)((h->n + kQuadEnvs - 1) / kQuadEnvs)), block(nw * 64);
     size_t lds = quad_lds_bytes(h->g);
+    if (h->lds_floor > lds) lds = h->lds_floor;  // diagnostics: caps workgroups per CU
+#define PE_QUAD(CC, RR, OW)                                                                 \
+  if (nw == 8)                                                                              \
+    hipLaunchKernelGGL((pe_step_quad<CC, RR, OW, 8>), grid, block, lds, s, a);              \
+  else                                                                                      \
+    hipLaunchKernelGGL((pe_step_quad<CC, RR, OW, 4>), grid, block, lds, s, a);
     switch (h->variant) {
-      case V_QUAD_C16R6_1W: hipLaunchKernelGGL((pe_step_quad<16, 6, true>), grid, block, lds, s, a); break;
-      case V_QUAD_C16R6: hipLaunchKernelGGL((pe_step_quad<16, 6, false>), grid, block, lds, s, a); break;
-      default: hipLaunchKernelGGL((pe_step_quad<64, 6, false>), grid, block, lds, s, a); break;
+      case V_QUAD_C16R6_1W: PE_QUAD(16, 6, true); break;
+      case V_QUAD_C16R6: PE_QUAD(16, 6, false); break;
+      default: PE_QUAD(64, 6, false); break;
     }
+#undef PE_QUAD
   } else {
     dim3 grid((unsigned)((h->n + kBlock - 1) / kBlock)), block(kBlock);
     size_t lds = lds_bytes(h->g);
@@ -1022,6 +1130,13 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   hipError_t he = hipGetDeviceCount(&ndev);
   if (he != hipSuccess || ndev == 0) return fail(PE_ERR_DEVICE, "no HIP device available (no CPU fallback)");
   if (device < 0 || device >= ndev) return fail(PE_ERR_ARG, "bad device index");
+  struct Restore {
+    int prev = -1;
+    ~Restore() {
+      if (prev >= 0) (void)hipSetDevice(prev);
+    }
+  } restore;
+  PE_HIP(hipGetDevice(&restore.prev));
   PE_HIP(hipSetDevice(device));
   hipDeviceProp_t prop;
   PE_HIP(hipGetDeviceProperties(&prop, device));
@@ -1042,8 +1157,9 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   g.GG = G * G;
   g.WPR = (2 * (G + 2 * R) + 63) / 64;
   g.NW = (4 * (G + 4) + 31) / 32 + 1;
+  if (g.NW < 4) g.NW = 4;  // 16-B visit rows: one dwordx4 per row in the sector kernel
   g.EW = (g.GG + 31) / 32;
-  g.gstride = (int64_t)G * g.WPR;
+  g.gstride = (int64_t)align_up((size_t)G * g.WPR, 2);  // 16-B aligned env blocks (row-pair loads)
   g.vstride = (int64_t)G * g.NW;
   g.hstride = (int64_t)align_up((size_t)g.GG, 8);
   g.estride = (int64_t)align_up((size_t)g.EW, 4);
@@ -1101,7 +1217,13 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   const bool lane_kernels = kenv && std::strcmp(kenv, "lane") == 0;
   if (!lane_kernels && h->variant != V_GENERIC) h->variant += V_QUAD_C16R6_1W - V_C16R6_1W;
   if (is_quad(h->variant) && quad_lds_bytes(g) > 160 * 1024) h->variant -= V_QUAD_C16R6_1W - V_C16R6_1W;
+  if (h->variant == V_QUAD_C16R6_1W && g.NW != 4) h->variant = V_C16R6_1W;  // needs 16-B visit rows
   h->kname = variant_name(h->variant);
+  const char* qw = std::getenv("PE_QUAD_WAVES");
+  h->quad_waves = (qw && std::atoi(qw) == 4) ? 4 : 8;
+  const char* lf = std::getenv("PE_LDS_FLOOR");
+  h->lds_floor = lf ? (size_t)std::strtoul(lf, nullptr, 10) : 0;
+  if (h->lds_floor > 160 * 1024) h->lds_floor = 160 * 1024;
 
   // one device allocation carved into 256-B aligned arrays
   const size_t n = (size_t)n_envs;
@@ -1118,7 +1240,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   const size_t o_ret = carve(n * sizeof(double));
   const size_t o_grid = carve(n * (size_t)g.gstride * 8);
   const size_t o_vis = carve(n * (size_t)g.vstride * 4);
-  const size_t o_v16 = carve(n * (size_t)g.hstride * 2);
+  const size_t o_vx = carve(n * (size_t)g.hstride * 4);
   const size_t o_expl = carve(n * (size_t)g.estride * 4);
   h->bytes = off;
   hipError_t me = hipMalloc(&h->mem, h->bytes);
@@ -1137,7 +1259,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   h->st.ep_ret = reinterpret_cast<double*>(base + o_ret);
   h->st.grid = reinterpret_cast<uint64_t*>(base + o_grid);
   h->st.vis = reinterpret_cast<uint32_t*>(base + o_vis);
-  h->st.v16 = reinterpret_cast<uint16_t*>(base + o_v16);
+  h->st.vx = reinterpret_cast<uint32_t*>(base + o_vx);
   h->st.expl = reinterpret_cast<uint32_t*>(base + o_expl);
   int rc = PE_OK;
   hipError_t e1 = hipMemset(h->mem, 0, h->bytes);
@@ -1169,7 +1291,8 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
 
 int pe_destroy(pe_handle* h) {
   if (!h) return PE_OK;
-  int rc = bind_device(h);
+  DeviceGuard dg(h);
+  int rc = dg.rc;
   if (rc == PE_OK && h->mem) {
     hipError_t e = hipFree(h->mem);
     if (e != hipSuccess) rc = hip_fail(e, "hipFree");
@@ -1183,8 +1306,8 @@ int pe_seed(pe_handle* h, uint64_t seed, int32_t reset_episode_counters) {
   h->rl.seed = seed;
   h->cfg.seed = seed;
   if (reset_episode_counters) {
-    int rc = bind_device(h);
-    if (rc) return rc;
+    DeviceGuard dg(h);
+    if (dg.rc) return dg.rc;
     // the episode counter is the 4th word of each packed scalar record
     PE_HIP(hipMemset2D(reinterpret_cast<char*>(h->st.scal) + 12, sizeof(uint4), 0, 4, (size_t)h->n));
   }
@@ -1193,8 +1316,8 @@ int pe_seed(pe_handle* h, uint64_t seed, int32_t reset_episode_counters) {
 
 int pe_reset(pe_handle* h, const uint8_t* mask, float* obs, void* stream) {
   if (!h) return fail(PE_ERR_ARG, "null handle");
-  int rc = bind_device(h);
-  if (rc) return rc;
+  DeviceGuard dg(h);
+  if (dg.rc) return dg.rc;
   StepArgs a = base_args(h);
   a.mask = mask;
   a.obs = obs;
@@ -1205,8 +1328,8 @@ int pe_step(pe_handle* h, const void* actions, int32_t action_bytes, float* obs,
             uint8_t* truncated, float* terminal_obs, double* ep_ret, int32_t* ep_len, void* stream) {
   if (!h || !actions || !obs || !reward || !terminated || !truncated) return fail(PE_ERR_ARG, "null argument");
   if (action_bytes != 4 && action_bytes != 8) return fail(PE_ERR_ARG, "action_bytes must be 4 or 8");
-  int rc = bind_device(h);
-  if (rc) return rc;
+  DeviceGuard dg(h);
+  if (dg.rc) return dg.rc;
   StepArgs a = base_args(h);
   a.act_bytes = action_bytes;
   a.actions = actions;
@@ -1222,8 +1345,8 @@ int pe_step(pe_handle* h, const void* actions, int32_t action_bytes, float* obs,
 
 int pe_get_info(pe_handle* h, int32_t* info, void* stream) {
   if (!h || !info) return fail(PE_ERR_ARG, "null argument");
-  int rc = bind_device(h);
-  if (rc) return rc;
+  DeviceGuard dg(h);
+  if (dg.rc) return dg.rc;
   StepArgs a = base_args(h);
   hipLaunchKernelGGL(pe_info_kernel, dim3((h->n + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream), a, info);
   PE_HIP(hipGetLastError());
@@ -1232,8 +1355,8 @@ int pe_get_info(pe_handle* h, int32_t* info, void* stream) {
 
 int pe_get_state(pe_handle* h, uint8_t* cells, int32_t* visits, int8_t* explored, int32_t* scalars, void* stream) {
   if (!h) return fail(PE_ERR_ARG, "null handle");
-  int rc = bind_device(h);
-  if (rc) return rc;
+  DeviceGuard dg(h);
+  if (dg.rc) return dg.rc;
   StepArgs a = base_args(h);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (cells || visits || explored) {
@@ -1252,8 +1375,8 @@ int pe_get_state(pe_handle* h, uint8_t* cells, int32_t* visits, int8_t* explored
 int pe_set_state(pe_handle* h, const uint8_t* cells, const int32_t* visits, const int8_t* explored,
                  const int32_t* scalars, void* stream) {
   if (!h) return fail(PE_ERR_ARG, "null handle");
-  int rc = bind_device(h);
-  if (rc) return rc;
+  DeviceGuard dg(h);
+  if (dg.rc) return dg.rc;
   StepArgs a = base_args(h);
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(pe_set_env_kernel, dim3((h->n + 127) / 128), dim3(128), 0, s, a, cells, visits, explored, scalars);
@@ -1265,8 +1388,8 @@ int pe_load_maps(pe_handle* h, int32_t k, const int32_t* env_index, const uint8_
                  float* obs_k, void* stream) {
   if (!h || (k > 0 && (!env_index || !cells || !rover))) return fail(PE_ERR_ARG, "null argument");
   if (k <= 0) return PE_OK;
-  int rc = bind_device(h);
-  if (rc) return rc;
+  DeviceGuard dg(h);
+  if (dg.rc) return dg.rc;
   StepArgs a = base_args(h);
   a.obs = obs_k;
   hipLaunchKernelGGL(pe_load_maps_kernel, dim3((k + kBlock - 1) / kBlock), dim3(kBlock), lds_bytes(h->g),
@@ -1277,8 +1400,8 @@ int pe_load_maps(pe_handle* h, int32_t k, const int32_t* env_index, const uint8_
 
 int pe_synth_actions(pe_handle* h, uint64_t seed, uint32_t t, int32_t* actions, void* stream) {
   if (!h || !actions) return fail(PE_ERR_ARG, "null argument");
-  int rc = bind_device(h);
-  if (rc) return rc;
+  DeviceGuard dg(h);
+  if (dg.rc) return dg.rc;
   hipLaunchKernelGGL(pe_synth_kernel, dim3((h->n + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream), h->n,
                      seed, h->rl.env_off, t, actions);
   PE_HIP(hipGetLastError());
@@ -1287,8 +1410,8 @@ int pe_synth_actions(pe_handle* h, uint64_t seed, uint32_t t, int32_t* actions, 
 
 int pe_poll_errors(pe_handle* h, int32_t* bits, void* stream) {
   if (!h || !bits) return fail(PE_ERR_ARG, "null argument");
-  int rc = bind_device(h);
-  if (rc) return rc;
+  DeviceGuard dg(h);
+  if (dg.rc) return dg.rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint32_t v = 0;
   PE_HIP(hipMemcpyAsync(&v, h->st.err_bits, sizeof(v), hipMemcpyDeviceToHost, s));
@@ -1297,6 +1420,15 @@ int pe_poll_errors(pe_handle* h, int32_t* bits, void* stream) {
   *bits = (int32_t)((v >> 2) & 7u);
   return PE_OK;
 }
+
+#ifdef PE_STAMPS
+int pe_debug_stamps(uint64_t* host, int64_t count) {
+  if (count > 16384 * 8) count = 16384 * 8;
+  PE_HIP(hipDeviceSynchronize());
+  PE_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), (size_t)count * 8, 0, hipMemcpyDeviceToHost));
+  return PE_OK;
+}
+#endif
 
 int32_t pe_num_envs(const pe_handle* h) { return h ? h->n : 0; }
 int32_t pe_kernel_variant(const pe_handle* h) { return h ? h->variant : -1; }

@@ -10,6 +10,9 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libplantos_hip.so")
+# diagnostics only (tools/ablate.py): load a differently built library
+if os.environ.get("PLANTOS_HIP_LIB"):
+    LIB_PATH = os.environ["PLANTOS_HIP_LIB"]
 
 PE_ABI_VERSION = 1
 PE_OK, PE_ERR_ARG, PE_ERR_DEVICE, PE_ERR_NOMEM, PE_ERR_NOROOM = 0, -1, -2, -3, -4

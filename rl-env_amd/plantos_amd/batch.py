@@ -57,6 +57,11 @@ class PlantOSBatch:
         self.episode_return = torch.zeros(n, dtype=torch.float64, device=dev)
         self.episode_length = torch.zeros(n, dtype=torch.int32, device=dev)
         self.info_buf = torch.zeros((n, C.PE_NINFO), dtype=torch.int32, device=dev)
+        self._dev_index = self.device.index or 0
+        self._L = L
+        self._out_ptrs = (self.reward.data_ptr(), self.terminated.data_ptr(), self.truncated.data_ptr())
+        self._tobs_ptr = self.terminal_obs.data_ptr()
+        self._ep_ptrs = (self.episode_return.data_ptr(), self.episode_length.data_ptr())
         self.raise_on_errors()
 
     def raise_on_errors(self):
@@ -115,20 +120,21 @@ class PlantOSBatch:
     def step(self, actions, obs=None, want_terminal_obs=True):
         """One step of every env. `actions`: int32/int64 tensor [n] on the device
         (other inputs are converted).  Returns device tensors
-        (obs, reward, terminated, truncated)."""
+        (obs, reward, terminated, truncated).  Asynchronous on torch's current
+        stream (graph-capturable); the library binds and restores the device."""
         a = actions
-        if not (isinstance(a, torch.Tensor) and a.device == self.device and a.dtype in (torch.int32, torch.int64)):
-            a = torch.as_tensor(a).to(device=self.device, dtype=torch.int64)
-        a = a.contiguous()
+        if not (type(a) is torch.Tensor and a.is_cuda and a.get_device() == self._dev_index
+                and (a.dtype is torch.int32 or a.dtype is torch.int64) and a.is_contiguous()):
+            a = torch.as_tensor(a).to(device=self.device, dtype=torch.int64).contiguous()
         if a.numel() != self.num_envs:
             raise ValueError(f"expected {self.num_envs} actions, got {a.numel()}")
         out = self.obs if obs is None else obs
-        with torch.cuda.device(self.device):
-            C.check(C.lib().pe_step(self.handle, _ptr(a), a.element_size(), _ptr(out), _ptr(self.reward),
-                                    _ptr(self.terminated), _ptr(self.truncated),
-                                    _ptr(self.terminal_obs) if want_terminal_obs else None,
-                                    _ptr(self.episode_return), _ptr(self.episode_length), self._stream()),
-                    "pe_step")
+        r, te, tr = self._out_ptrs
+        rc = self._L.pe_step(self.handle, a.data_ptr(), a.element_size(), out.data_ptr(), r, te, tr,
+                             self._tobs_ptr if want_terminal_obs else None, self._ep_ptrs[0], self._ep_ptrs[1],
+                             torch.cuda.current_stream(self._dev_index).cuda_stream)
+        if rc:
+            C.check(rc, "pe_step")
         return out, self.reward, self.terminated, self.truncated
 
     # ----------------------------------------------------------------- inspection
