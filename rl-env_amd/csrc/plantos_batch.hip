@@ -1220,7 +1220,8 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   if (h->variant == V_QUAD_C16R6_1W && g.NW != 4) h->variant = V_C16R6_1W;  // needs 16-B visit rows
   h->kname = variant_name(h->variant);
   const char* qw = std::getenv("PE_QUAD_WAVES");
-  h->quad_waves = (qw && std::atoi(qw) == 4) ? 4 : 8;
+  // measured (profiles/r1c-r1e): 4 waves win at C=16, 8 waves at C=64
+  h->quad_waves = qw ? (std::atoi(qw) == 4 ? 4 : 8) : (C >= 64 ? 8 : 4);
   const char* lf = std::getenv("PE_LDS_FLOOR");
   h->lds_floor = lf ? (size_t)std::strtoul(lf, nullptr, 10) : 0;
   if (h->lds_floor > 160 * 1024) h->lds_floor = 160 * 1024;
