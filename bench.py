@@ -69,7 +69,7 @@ def cpu_baseline(args, plants, obstacles):
     n_envs = min(args.envs, 65536)
     secs, _ = O.bench(cfg, n_envs, 10, args.seed, threads)  # calibration
     rate = n_envs * 10 / max(secs, 1e-6)
-    steps = int(max(10, min(2000, args.cpu_seconds * rate / n_envs)))
+    steps = int(max(10, min(20000, args.cpu_seconds * rate / n_envs)))
     secs, _ = O.bench(cfg, n_envs, steps, args.seed, threads)
     return {"value": n_envs * steps / secs, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": f"{n_envs} envs x {steps} steps ({secs:.1f} s) of the same synthetic workload, "
@@ -117,20 +117,21 @@ def main():
     plants = args.plants if args.plants is not None else (10 if G <= 32 else 100)
     obstacles = args.obstacles if args.obstacles is not None else (12 if G <= 32 else 120)
     n = args.envs
-    b = PlantOSBatch(n, grid_size=G, num_plants=plants, num_obstacles=obstacles, lidar_range=R,
-                     lidar_channels=C, seed=args.seed, env_id_offset=rank * n, device=device)
+    from plantos_amd.shard import ShardedPlantOS
+
+    # rank r owns global env ids [r*n, (r+1)*n) (env_id_offset), no data-path collective
+    shard = ShardedPlantOS(n, seed=args.seed, batch_factory=lambda n_, **kw: PlantOSBatch(
+        n_, grid_size=G, num_plants=plants, num_obstacles=obstacles, lidar_range=R, lidar_channels=C,
+        device=device, **kw))
+    b = shard.batch
     T = args.action_steps
     actions = torch.empty((T, n), dtype=torch.int32, device=device)
     for t in range(T):
         b.synth_actions(args.seed, t, out=actions[t])
-    gather_bufs = None
-    if args.gather and world > 1:
-        gather_bufs = [torch.empty_like(b.obs) for _ in range(world)] if rank == 0 else None
-
     def one_step(t):
         b.step(actions[t % T])
         if args.gather and world > 1:
-            dist.gather(b.obs, gather_bufs, dst=0)
+            shard.gather_outputs(root=0)  # RCCL gather of (obs, reward, term, trunc) to rank 0
 
     for t in range(args.warmup):
         one_step(t)

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PE_ABI_VERSION 1
+#define PE_ABI_VERSION 2
 
 enum pe_status {
     PE_OK = 0,
@@ -118,10 +118,14 @@ int pe_reset(pe_handle* h, const uint8_t* mask_or_null, float* obs, void* stream
  *   terminated   u8[n], truncated u8[n]
  *   terminal_obs f32[n, D] or NULL: rows of done envs receive the pre-reset obs
  *   episode_return f64[n] or NULL: rows of done envs receive the episode's f64 return
- *   episode_length i32[n] or NULL: rows of done envs receive the episode length      */
+ *   episode_length i32[n] or NULL: rows of done envs receive the episode length
+ *   terminal_info  i32[n, PE_NINFO] or NULL: rows of done envs receive _get_info of the
+ *                  final (pre-reset) state (DummyVecEnv keeps that step's info dict)
+ * Only rows of done envs are written in the four terminal outputs (autoreset on).   */
 int pe_step(pe_handle* h, const void* actions, int32_t action_bytes, float* obs, float* reward,
             uint8_t* terminated, uint8_t* truncated, float* terminal_obs_or_null,
-            double* episode_return_or_null, int32_t* episode_length_or_null, void* stream);
+            double* episode_return_or_null, int32_t* episode_length_or_null,
+            int32_t* terminal_info_or_null, void* stream);
 
 /* info columns (pe_info) for all envs: int32[n, PE_NINFO]. */
 int pe_get_info(pe_handle* h, int32_t* info, void* stream);

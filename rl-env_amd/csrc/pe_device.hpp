@@ -235,6 +235,30 @@ __device__ __forceinline__ bool expl_test_set(const State& st, const Geo& g, int
   return true;
 }
 
+// _get_info (plantos_env.py:317-336), integer columns (pe_info layout of
+// include/plantos_batch.h) for env e with scalars s.
+__device__ inline void write_info(const State& st, const Geo& g, int64_t e, const Scal& s, int32_t* o) {
+  int th = 0, hy = 0;
+  for (int row = 0; row < g.G; ++row)
+    for (int w = 0; w < g.WPR; ++w) {
+      const uint64_t v = st.grid[e * g.gstride + (int64_t)row * g.WPR + w];
+      const uint64_t lo = v & kEven64, hi = (v >> 1) & kEven64, real = st.tab->grid_real[w];
+      th += __popcll(lo & hi & real);   // sum(plants.values())           :318
+      hy += __popcll(~lo & hi & real);  // len(plants) - thirsty          :319
+    }
+  o[0] = s.x;                                 // rover_position           :324
+  o[1] = s.y;
+  o[2] = th;
+  o[3] = hy;
+  o[4] = th + hy;                             // total_plants             :327
+  o[5] = s.step;                              // step_count               :328
+  o[6] = s.expl;                              // explored_cells           :320
+  o[7] = s.total;                             // total_cells              :321
+  o[8] = (s.flags & F_COLLIDED) ? 1 : 0;      // collided_with_wall       :333
+  o[9] = s.coll;                              // total_collisions         :334
+  o[10] = (int)((s.flags >> 2) & 7u);         // error flags (PE_S_POISONED layout)
+}
+
 // ------------------------------------------------------------------ map generation
 // Index of the j-th real cell (row-major) whose code matches `kind`
 // (kind 0: not an obstacle, kind 1: empty).  Returns the cell id x*G+y.

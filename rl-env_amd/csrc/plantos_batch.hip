@@ -43,6 +43,7 @@ struct StepArgs {
   float* tobs;
   double* ep_ret_out;
   int32_t* ep_len_out;
+  int32_t* tinfo;       // terminal _get_info rows of done envs (may be NULL)
   const uint8_t* mask;  // reset kernel
 };
 
@@ -204,6 +205,7 @@ __global__ __launch_bounds__(kBlock) void pe_step_kernel(StepArgs a) {
       }
       if (a.ep_ret_out) a.ep_ret_out[e] = ret;
       if (a.ep_len_out) a.ep_len_out[e] = s.step;
+      if (a.tinfo) write_info(a.st, a.g, e, s, a.tinfo + e * PE_NINFO);
       s = reset_env(a.st, a.g, a.rl, e, s.episode);
       ret = 0.0;
     }
@@ -366,6 +368,7 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
       }
       if (a.ep_ret_out) a.ep_ret_out[e] = ret;
       if (a.ep_len_out) a.ep_len_out[e] = s.step;
+      if (a.tinfo) write_info(a.st, a.g, e, s, a.tinfo + e * PE_NINFO);
       s = reset_env(st, g, rl, e, s.episode);
       st.ep_ret[e] = 0.0;
       st.scal[e] = pack(s);
@@ -690,6 +693,7 @@ __global__ __launch_bounds__(64 * NW) void pe_step_quad(StepArgs a) {
       }
       if (a.ep_ret_out) a.ep_ret_out[e] = ret;
       if (a.ep_len_out) a.ep_len_out[e] = s.step;
+      if (a.tinfo) write_info(a.st, a.g, e, s, a.tinfo + e * PE_NINFO);
       s = reset_env(st, g, rl, e, s.episode);
       st.ep_ret[e] = 0.0;
       st.scal[e] = pack(s);
@@ -781,27 +785,8 @@ __global__ void pe_info_kernel(StepArgs a, int32_t* info) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= a.n) return;
   const Geo& g = a.g;
-  Scal s = unpack(a.st.scal[e]);
-  int th = 0, hy = 0;
-  for (int row = 0; row < g.G; ++row)
-    for (int w = 0; w < g.WPR; ++w) {
-      uint64_t v = a.st.grid[e * g.gstride + (int64_t)row * g.WPR + w];
-      uint64_t lo = v & kEven64, hi = (v >> 1) & kEven64, real = a.st.tab->grid_real[w];
-      th += __popcll(lo & hi & real);
-      hy += __popcll(~lo & hi & real);
-    }
-  int32_t* o = info + e * PE_NINFO;
-  o[PE_I_X] = s.x;
-  o[PE_I_Y] = s.y;
-  o[PE_I_THIRSTY] = th;
-  o[PE_I_HYDRATED] = hy;
-  o[PE_I_TOTAL_PLANTS] = th + hy;
-  o[PE_I_STEP] = s.step;
-  o[PE_I_EXPLORED] = s.expl;
-  o[PE_I_TOTAL_CELLS] = s.total;
-  o[PE_I_COLLIDED] = (s.flags & F_COLLIDED) ? 1 : 0;
-  o[PE_I_COLLISIONS] = s.coll;
-  o[PE_I_POISONED] = (int)((s.flags >> 2) & 7u);
+  static_assert(PE_NINFO == 11 && PE_I_POISONED == 10, "write_info column layout");
+  write_info(a.st, g, e, unpack(a.st.scal[e]), info + e * PE_NINFO);
 }
 
 // get_state: one thread per (env, cell).
@@ -1326,7 +1311,8 @@ int pe_reset(pe_handle* h, const uint8_t* mask, float* obs, void* stream) {
 }
 
 int pe_step(pe_handle* h, const void* actions, int32_t action_bytes, float* obs, float* reward, uint8_t* terminated,
-            uint8_t* truncated, float* terminal_obs, double* ep_ret, int32_t* ep_len, void* stream) {
+            uint8_t* truncated, float* terminal_obs, double* ep_ret, int32_t* ep_len, int32_t* terminal_info,
+            void* stream) {
   if (!h || !actions || !obs || !reward || !terminated || !truncated) return fail(PE_ERR_ARG, "null argument");
   if (action_bytes != 4 && action_bytes != 8) return fail(PE_ERR_ARG, "action_bytes must be 4 or 8");
   DeviceGuard dg(h);
@@ -1341,6 +1327,7 @@ int pe_step(pe_handle* h, const void* actions, int32_t action_bytes, float* obs,
   a.tobs = terminal_obs;
   a.ep_ret_out = ep_ret;
   a.ep_len_out = ep_len;
+  a.tinfo = terminal_info;
   return launch_step(h, a, static_cast<hipStream_t>(stream));
 }
 

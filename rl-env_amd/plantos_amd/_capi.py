@@ -14,13 +14,15 @@ LIB_PATH = os.path.join(HERE, "libplantos_hip.so")
 if os.environ.get("PLANTOS_HIP_LIB"):
     LIB_PATH = os.environ["PLANTOS_HIP_LIB"]
 
-PE_ABI_VERSION = 1
+PE_ABI_VERSION = 2
 PE_OK, PE_ERR_ARG, PE_ERR_DEVICE, PE_ERR_NOMEM, PE_ERR_NOROOM = 0, -1, -2, -3, -4
 PE_NSCAL = 8
 PE_NINFO = 11
 (PE_S_X, PE_S_Y, PE_S_STEP, PE_S_COLL, PE_S_COLLIDED, PE_S_BONUS, PE_S_POISONED, PE_S_EPISODE) = range(8)
 (PE_I_X, PE_I_Y, PE_I_THIRSTY, PE_I_HYDRATED, PE_I_TOTAL_PLANTS, PE_I_STEP, PE_I_EXPLORED,
  PE_I_TOTAL_CELLS, PE_I_COLLIDED, PE_I_COLLISIONS, PE_I_POISONED) = range(11)
+
+PE_CELL_EMPTY, PE_CELL_OBSTACLE, PE_CELL_HYDRATED, PE_CELL_THIRSTY = range(4)
 
 # exported symbols (tests/test_capi_symbols.py checks they match include/plantos_batch.h)
 EXPORTS = [
@@ -69,7 +71,7 @@ def lib():
     L.pe_destroy.argtypes = [P]
     L.pe_seed.argtypes = [P, U64, I32]
     L.pe_reset.argtypes = [P, P, P, P]
-    L.pe_step.argtypes = [P, P, I32, P, P, P, P, P, P, P, P]
+    L.pe_step.argtypes = [P, P, I32, P, P, P, P, P, P, P, P, P]
     L.pe_get_info.argtypes = [P, P, P]
     L.pe_get_state.argtypes = [P, P, P, P, P, P]
     L.pe_set_state.argtypes = [P, P, P, P, P, P]

@@ -57,11 +57,13 @@ class PlantOSBatch:
         self.episode_return = torch.zeros(n, dtype=torch.float64, device=dev)
         self.episode_length = torch.zeros(n, dtype=torch.int32, device=dev)
         self.info_buf = torch.zeros((n, C.PE_NINFO), dtype=torch.int32, device=dev)
+        self.terminal_info = torch.zeros((n, C.PE_NINFO), dtype=torch.int32, device=dev)
         self._dev_index = self.device.index or 0
         self._L = L
         self._out_ptrs = (self.reward.data_ptr(), self.terminated.data_ptr(), self.truncated.data_ptr())
         self._tobs_ptr = self.terminal_obs.data_ptr()
-        self._ep_ptrs = (self.episode_return.data_ptr(), self.episode_length.data_ptr())
+        self._ep_ptrs = (self.episode_return.data_ptr(), self.episode_length.data_ptr(),
+                         self.terminal_info.data_ptr())
         self.raise_on_errors()
 
     def raise_on_errors(self):
@@ -132,7 +134,7 @@ class PlantOSBatch:
         r, te, tr = self._out_ptrs
         rc = self._L.pe_step(self.handle, a.data_ptr(), a.element_size(), out.data_ptr(), r, te, tr,
                              self._tobs_ptr if want_terminal_obs else None, self._ep_ptrs[0], self._ep_ptrs[1],
-                             torch.cuda.current_stream(self._dev_index).cuda_stream)
+                             self._ep_ptrs[2], torch.cuda.current_stream(self._dev_index).cuda_stream)
         if rc:
             C.check(rc, "pe_step")
         return out, self.reward, self.terminated, self.truncated

@@ -40,3 +40,104 @@ class OracleVec:
             fresh = self.b.obs(np.nonzero(done)[0])
             obs[done] = fresh[done]
         return obs, rew, te, tr, term_obs, ep_ret, ep_len
+
+
+class OracleBatch:
+    """CPU stand-in with PlantOSBatch's interface, backed by the oracle (TEST INFRA:
+    lets the host-side vec-env logic run and be checked without a GPU)."""
+
+    def __init__(self, n, grid_size, num_plants, num_obstacles, lidar_range, lidar_channels, seed=0,
+                 max_steps=1000):
+        import torch
+        self.torch = torch
+        self.device = torch.device("cpu")
+        self.num_envs = n
+        self.grid_size = grid_size
+        self.cfg_t = (grid_size, num_plants, num_obstacles, lidar_range, lidar_channels)
+        self.ov = OracleVec(self.cfg_t, np.arange(n), seed, max_steps=max_steps)
+        self.obs_dim = O.obs_dim(self.ov.cfg)
+        D = self.obs_dim
+        self.obs = torch.as_tensor(self.ov.obs())
+        self.reward = torch.zeros(n, dtype=torch.float32)
+        self.terminated = torch.zeros(n, dtype=torch.uint8)
+        self.truncated = torch.zeros(n, dtype=torch.uint8)
+        self.terminal_obs = torch.zeros((n, D), dtype=torch.float32)
+        self.episode_return = torch.zeros(n, dtype=torch.float64)
+        self.episode_length = torch.zeros(n, dtype=torch.int32)
+        self.terminal_info = torch.zeros((n, 11), dtype=torch.int32)
+        self.seed_value = seed
+
+    def _info_rows(self):
+        b = self.ov.b
+        rows = np.zeros((self.num_envs, 11), np.int32)
+        for e in range(self.num_envs):
+            th, hy, tot, ex, tc = b.info(e)
+            s = b.scal[e]
+            rows[e] = [s[O.S_X], s[O.S_Y], th, hy, tot, s[O.S_STEP], ex, tc, s[O.S_COLLIDED], s[O.S_COLL],
+                       s[O.S_POISONED]]
+        return rows
+
+    def reset(self, mask=None):
+        for e in range(self.num_envs):
+            if mask is None or mask[e]:
+                self.ov.b.reset_philox(e, self.ov.seed, int(self.ov.ids[e]), int(self.ov.b.scal[e, O.S_EPISODE]))
+                self.ov.ret[e] = 0.0
+        self.obs = self.torch.as_tensor(self.ov.obs())
+        return self.obs
+
+    def step(self, actions):
+        a = np.asarray(actions.cpu().numpy() if hasattr(actions, "cpu") else actions, np.int64)
+        pre_info = None
+        obs, rew, te, tr, tobs, ret, ln = None, None, None, None, None, None, None
+        # terminal info = info of the post-step, pre-reset state: step without reset first
+        b = self.ov.b
+        o, r, t1, t2 = b.step(a)
+        pre_info = self._info_rows()
+        done = t1 | t2
+        self.ov.ret += r
+        ret = self.ov.ret.copy()
+        ln = b.scal[:, O.S_STEP].copy()
+        tobs = o.copy()
+        for k in np.nonzero(done)[0]:
+            b.reset_philox(int(k), self.ov.seed, int(self.ov.ids[k]), int(b.scal[k, O.S_EPISODE]))
+            self.ov.ret[k] = 0.0
+        if done.any():
+            o[done] = b.obs(np.nonzero(done)[0])[done]
+        T = self.torch
+        self.obs = T.as_tensor(o)
+        self.reward = T.as_tensor(r.astype(np.float32))
+        self.terminated = T.as_tensor(t1.astype(np.uint8))
+        self.truncated = T.as_tensor(t2.astype(np.uint8))
+        self.terminal_obs[done] = T.as_tensor(tobs[done])
+        self.episode_return[done] = T.as_tensor(ret[done])
+        self.episode_length[done] = T.as_tensor(ln[done].astype(np.int32))
+        self.terminal_info[done] = T.as_tensor(pre_info[done])
+        return self.obs, self.reward, self.terminated, self.truncated
+
+    def get_info(self):
+        return self.torch.as_tensor(self._info_rows())
+
+    def get_state(self):
+        b = self.ov.b
+        T = self.torch
+        return {"cells": T.as_tensor(b.cells.copy()), "visits": T.as_tensor(b.visits.copy()),
+                "explored": T.as_tensor(b.explored.copy()), "scalars": T.as_tensor(b.scal.copy())}
+
+    def set_state(self, cells=None, visits=None, explored=None, scalars=None):
+        b = self.ov.b
+        if cells is not None:
+            b.cells[...] = np.asarray(cells)
+        if visits is not None:
+            b.visits[...] = np.asarray(visits)
+        if explored is not None:
+            b.explored[...] = np.asarray(explored)
+        if scalars is not None:
+            b.scal[...] = np.asarray(scalars)
+
+    def seed(self, seed, reset_episode_counters=True):
+        self.ov.seed = seed
+        if reset_episode_counters:
+            self.ov.b.scal[:, O.S_EPISODE] = 0
+
+    def close(self):
+        pass

@@ -1,0 +1,60 @@
+"""GPU: the SB3-protocol drop-in (PlantOSVecEnv over the HIP batch) against the
+same adapter over the oracle batch -- obs, rewards, dones and every info dict,
+across auto-resets (terminal_observation, TimeLimit.truncated, episode)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle_rollout import OracleBatch
+from plantos_amd import PlantOSVecEnv, PlantOSVectorEnv
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("cfg,n,T,max_steps", [
+    (dict(grid_size=20, num_plants=10, num_obstacles=12, lidar_range=6, lidar_channels=16), 96, 130, 60),
+    (dict(grid_size=25, num_plants=10, num_obstacles=12, lidar_range=6, lidar_channels=16), 70, 70, 30),
+    (dict(grid_size=7, num_plants=3, num_obstacles=3, lidar_range=3, lidar_channels=12), 33, 50, 20),
+])
+def test_vec_env_gpu_vs_oracle(cfg, n, T, max_steps):
+    seed = 21
+    gpu = PlantOSVecEnv(n, seed=seed, max_steps=max_steps, device="cuda:0", **cfg)
+    ref = PlantOSVecEnv(n, batch=OracleBatch(n, seed=seed, max_steps=max_steps, **cfg), max_steps=max_steps, **cfg)
+    o1, o2 = gpu.reset(), ref.reset()
+    assert (o1 == o2).all()
+    for i in (0, n - 1):
+        assert gpu.reset_infos[i] == ref.reset_infos[i]
+    rng = np.random.default_rng(3)
+    for t in range(T):
+        a = rng.integers(0, 5, n)
+        g_obs, g_rew, g_done, g_inf = gpu.step(a)
+        r_obs, r_rew, r_done, r_inf = ref.step(a)
+        assert (g_obs == r_obs).all() and (g_rew == r_rew).all() and (g_done == r_done).all(), t
+        for e in list(np.nonzero(r_done)[0]) + [0, n // 2]:
+            gd, rd = g_inf[e], r_inf[e]
+            assert gd.keys() == rd.keys()
+            for k in gd:
+                if k == "terminal_observation":
+                    assert (gd[k] == rd[k]).all()
+                elif k == "episode":
+                    assert gd[k]["r"] == rd[k]["r"] and gd[k]["l"] == rd[k]["l"]
+                else:
+                    assert gd[k] == rd[k], (t, e, k)
+    assert gpu.get_attr("visit_counts", [5])[0].tolist() == ref.get_attr("visit_counts", [5])[0].tolist()
+    gpu.close()
+
+
+def test_vec_env_tensor_mode_and_gym_face():
+    cfg = dict(grid_size=20, num_plants=10, num_obstacles=12, lidar_range=6, lidar_channels=16)
+    v = PlantOSVecEnv(64, tensors=True, device="cuda:0", **cfg)
+    obs = v.reset()
+    assert isinstance(obs, torch.Tensor) and obs.is_cuda and obs.shape == (64, 107)
+    o, r, d, inf = v.step(torch.zeros(64, dtype=torch.int64, device="cuda:0"))
+    assert o.is_cuda and r.dtype == torch.float32 and d.dtype == torch.bool
+    v.close()
+    g = PlantOSVectorEnv(8, max_steps=5, device="cuda:0", **cfg)
+    g.reset(seed=3)
+    for t in range(5):
+        obs, rew, term, trunc, infos = g.step(np.full(8, t % 5))
+    assert trunc.all() and infos["_final_info"].all()
+    g.close()
