@@ -237,12 +237,13 @@ __device__ __forceinline__ bool expl_test_set(const State& st, const Geo& g, int
 
 // _get_info (plantos_env.py:317-336), integer columns (pe_info layout of
 // include/plantos_batch.h) for env e with scalars s.
-__device__ inline void write_info(const State& st, const Geo& g, int64_t e, const Scal& s, int32_t* o) {
+__device__ inline void write_info(const State& st, const Geo& g, const Tables* tab, int64_t e, const Scal& s,
+                                  int32_t* o) {
   int th = 0, hy = 0;
   for (int row = 0; row < g.G; ++row)
     for (int w = 0; w < g.WPR; ++w) {
       const uint64_t v = st.grid[e * g.gstride + (int64_t)row * g.WPR + w];
-      const uint64_t lo = v & kEven64, hi = (v >> 1) & kEven64, real = st.tab->grid_real[w];
+      const uint64_t lo = v & kEven64, hi = (v >> 1) & kEven64, real = tab->grid_real[w];
       th += __popcll(lo & hi & real);   // sum(plants.values())           :318
       hy += __popcll(~lo & hi & real);  // len(plants) - thirsty          :319
     }
@@ -260,19 +261,32 @@ __device__ inline void write_info(const State& st, const Geo& g, int64_t e, cons
 }
 
 // ------------------------------------------------------------------ map generation
+// A "grid image" is one env's grid rows [G][WPR] (padded 2-bit codes) anywhere:
+// the env's block in HBM, or a scratch copy in LDS during an in-kernel reset.
+__device__ __forceinline__ int img_code(const uint64_t* sg, const Geo& g, int row, int pcol) {
+  const int bit = 2 * pcol;
+  return (int)((sg[row * g.WPR + (bit >> 6)] >> (bit & 63)) & 3u);
+}
+
+__device__ __forceinline__ void img_set(uint64_t* sg, const Geo& g, int row, int pcol, int code) {
+  const int bit = 2 * pcol;
+  uint64_t& w = sg[row * g.WPR + (bit >> 6)];
+  w = (w & ~(3ull << (bit & 63))) | ((uint64_t)code << (bit & 63));
+}
+
 // Index of the j-th real cell (row-major) whose code matches `kind`
 // (kind 0: not an obstacle, kind 1: empty).  Returns the cell id x*G+y.
-__device__ inline int nth_cell(const State& st, const Geo& g, int64_t e, int j, int kind) {
+__device__ inline int img_nth_cell(const uint64_t* sg, const Geo& g, const Tables* tab, int j, int kind) {
   for (int row = 0; row < g.G; ++row) {
     for (int w = 0; w < g.WPR; ++w) {
-      uint64_t v = st.grid[e * g.gstride + (int64_t)row * g.WPR + w];
-      uint64_t lo = v & kEven64, hi = (v >> 1) & kEven64;
-      uint64_t real = st.tab->grid_real[w];
+      const uint64_t v = sg[row * g.WPR + w];
+      const uint64_t lo = v & kEven64, hi = (v >> 1) & kEven64;
+      const uint64_t real = tab->grid_real[w];
       uint64_t m = kind == 0 ? (real & ~(lo & ~hi)) : (real & ~(lo | hi));
-      int c = __popcll(m);
+      const int c = __popcll(m);
       if (j < c) {
         for (int k = 0; k < j; ++k) m &= m - 1;
-        int pcol = w * 32 + (__ffsll((unsigned long long)m) - 1) / 2;
+        const int pcol = w * 32 + (__ffsll((unsigned long long)m) - 1) / 2;
         return row * g.G + (pcol - g.R);
       }
       j -= c;
@@ -281,39 +295,35 @@ __device__ inline int nth_cell(const State& st, const Geo& g, int64_t e, int j, 
   return 0;  // unreachable when j < count
 }
 
-// reset() for one env (plantos_env.py:125-158, _generate_map 338-372) in the
-// device-rng mode defined by oracle po_reset_philox: Philox stream keyed by
-// (seed, global env id, episode); candidate lists in row-major order.
-// Writes all state of env e; returns the new scalars.
-__device__ inline Scal reset_env(const State& st, const Geo& g, const Rules& rl, int64_t e, uint32_t episode) {
+// _generate_map (plantos_env.py:338-372) in the device-rng mode defined by
+// oracle po_reset_philox: Philox stream keyed by (seed, global env id, episode),
+// candidate lists in row-major order.  Writes the grid image sg (all rows) and
+// returns the new scalars of the episode (flags F_NOROOM if there is no room,
+// plantos_env.py:360-364).  picks: P u16 of scratch.
+__device__ inline Scal gen_map(const Geo& g, const Rules& rl, const Tables* tab, uint64_t* sg, uint16_t* picks,
+                               uint32_t env_id, uint32_t episode) {
   const int G = g.G;
-  // clear
-  for (int row = 0; row < G; ++row) {
-    for (int w = 0; w < g.WPR; ++w) st.grid[e * g.gstride + (int64_t)row * g.WPR + w] = st.tab->grid_pad[w];
-    for (int w = 0; w < g.NW; ++w) st.vis[e * g.vstride + (int64_t)row * g.NW + w] = st.tab->vis_pad[w];
-  }
-  // vx and the explored bitmap are not cleared: every nibble is now 0 (vx is
-  // read only behind a nibble of 15) and a fresh episode is in derived-explored mode.
-
+  for (int row = 0; row < G; ++row)
+    for (int w = 0; w < g.WPR; ++w) sg[row * g.WPR + w] = tab->grid_pad[w];
   Stream rng;
-  rng.init(rl.seed, rl.env_off + (uint32_t)e, episode);
+  rng.init(rl.seed, env_id, episode);
   // obstacle clusters, plantos_env.py:341-354
   const int clusters = rl.O / 3;
   for (int q = 0; q < clusters; ++q) {
-    int cx = 2 + (int)rng.below((uint32_t)(G - 4));
-    int cy = 2 + (int)rng.below((uint32_t)(G - 4));
-    int size = 2 + (int)rng.below(2u);
+    const int cx = 2 + (int)rng.below((uint32_t)(G - 4));
+    const int cy = 2 + (int)rng.below((uint32_t)(G - 4));
+    const int size = 2 + (int)rng.below(2u);
     for (int dx = 0; dx < size; ++dx)
       for (int dy = 0; dy < size; ++dy) {
-        int ox = cx + dx - size / 2, oy = cy + dy - size / 2;
-        if (0 <= ox && ox < G && 0 <= oy && oy < G) grid_set(st, g, e, ox, oy + g.R, OBST);
+        const int ox = cx + dx - size / 2, oy = cy + dy - size / 2;
+        if (0 <= ox && ox < G && 0 <= oy && oy < G) img_set(sg, g, ox, oy + g.R, OBST);
       }
   }
   int n_obst = 0;
   for (int row = 0; row < G; ++row)
     for (int w = 0; w < g.WPR; ++w) {
-      uint64_t v = st.grid[e * g.gstride + (int64_t)row * g.WPR + w];
-      n_obst += __popcll(v & ~(v >> 1) & st.tab->grid_real[w] & kEven64);
+      const uint64_t v = sg[row * g.WPR + w];
+      n_obst += __popcll(v & ~(v >> 1) & tab->grid_real[w] & kEven64);
     }
   const int nfree = g.GG - n_obst;
   Scal s;
@@ -328,32 +338,65 @@ __device__ inline Scal reset_env(const State& st, const Geo& g, const Rules& rl,
     s.x = 0;
     s.y = 0;
     s.expl = 0;
-    atomicOr(st.err_bits, F_NOROOM);
     return s;
   }
   // random.sample(list(available), P): set-based selection, row-major list
-  uint32_t* picks = st.vx + e * g.hstride;  // scratch: pick order (all nibbles are 0 here)
   for (int i = 0; i < rl.P; ++i) {
     int c;
     for (;;) {
-      int j = (int)rng.below((uint32_t)nfree);
-      c = nth_cell(st, g, e, j, 0);
-      if (grid_code(st, g, e, c / G, c % G + g.R) == EMPTY) break;  // else already selected
+      c = img_nth_cell(sg, g, tab, (int)rng.below((uint32_t)nfree), 0);
+      if (img_code(sg, g, c / G, c % G + g.R) == EMPTY) break;  // else already selected
     }
-    grid_set(st, g, e, c / G, c % G + g.R, HYD);
-    picks[i] = (uint32_t)c;
+    img_set(sg, g, c / G, c % G + g.R, HYD);
+    picks[i] = (uint16_t)c;
   }
   // thirsty draws in sample order, plantos_env.py:367-369
   for (int i = 0; i < rl.P; ++i) {
-    int c = picks[i];
-    if (rng.random53() < rl.p_thirsty) grid_set(st, g, e, c / G, c % G + g.R, THIRSTY);
+    const int c = picks[i];
+    if (rng.random53() < rl.p_thirsty) img_set(sg, g, c / G, c % G + g.R, THIRSTY);
   }
   // rover: choice(list(available - plants)), plantos_env.py:370-372
-  int rc = nth_cell(st, g, e, (int)rng.below((uint32_t)(nfree - rl.P)), 1);
+  const int rc = img_nth_cell(sg, g, tab, (int)rng.below((uint32_t)(nfree - rl.P)), 1);
   s.x = rc / G;
   s.y = rc % G;
-  vis_set(st, g, e, s.x, s.y, 1u);  // visit[rover] = 1 (plantos_env.py:146-147); explored[rover]
-  return s;                         // = 2 follows from it (plantos_env.py:236)
+  return s;
+}
+
+// Fresh visit rows of env e (all zero, pads 10) with visit[rover] = 1
+// (plantos_env.py:146-147; explored[rover] = 2 follows from it, :236).  The
+// overflow slots and the explored bitmap are not cleared: every nibble is now 0
+// (vx is read only behind a nibble of 15) and a fresh episode is in derived mode.
+__device__ inline void reset_visits(const State& st, const Geo& g, const Tables* tab, int64_t e, const Scal& s) {
+  for (int row = 0; row < g.G; ++row)
+    for (int w = 0; w < g.NW; ++w) st.vis[e * g.vstride + (int64_t)row * g.NW + w] = tab->vis_pad[w];
+  if (!(s.flags & F_NOROOM)) vis_set(st, g, e, s.x, s.y, 1u);
+}
+
+// reset() for one env (plantos_env.py:125-158), generated in place in HBM.
+// tab: the handle's tables, ideally a copy in LDS (read in every scan step).
+__device__ inline Scal reset_env(const State& st, const Geo& g, const Rules& rl, const Tables* tab, int64_t e,
+                                 uint32_t episode) {
+  uint16_t* picks = reinterpret_cast<uint16_t*>(st.vx + e * g.hstride);  // scratch (all nibbles 0 after)
+  const Scal s = gen_map(g, rl, tab, st.grid + e * g.gstride, picks, rl.env_off + (uint32_t)e, episode);
+  if (s.flags & F_NOROOM) atomicOr(st.err_bits, F_NOROOM);
+  reset_visits(st, g, tab, e, s);
+  return s;
+}
+
+// Bytes of LDS scratch reset_env_scratch needs (grid image + picks, 8-B aligned).
+__host__ __device__ constexpr int reset_scratch_bytes(int G, int WPR, int P) { return 8 + G * WPR * 8 + 2 * P; }
+
+// reset() generated in a scratch image (LDS) and written to HBM row by row:
+// the rejection-sampling scans run at LDS latency instead of HBM latency.
+__device__ inline Scal reset_env_scratch(const State& st, const Geo& g, const Rules& rl, const Tables* tab, int64_t e,
+                                         uint32_t episode, uint64_t* sg) {
+  uint16_t* picks = reinterpret_cast<uint16_t*>(sg + g.G * g.WPR);
+  const Scal s = gen_map(g, rl, tab, sg, picks, rl.env_off + (uint32_t)e, episode);
+  if (s.flags & F_NOROOM) atomicOr(st.err_bits, F_NOROOM);
+  uint64_t* gb = st.grid + e * g.gstride;
+  for (int k = 0; k < g.G * g.WPR; ++k) gb[k] = sg[k];
+  reset_visits(st, g, tab, e, s);
+  return s;
 }
 
 }  // namespace pe

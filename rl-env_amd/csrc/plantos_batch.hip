@@ -26,7 +26,8 @@ using namespace pe;
 namespace {
 
 constexpr int kBlock = 64;      // envs per workgroup (one wave)
-constexpr int kTabFloats = 344; // Tables::dist + pos + vis
+constexpr int kTabFloats = (int)(sizeof(Tables) / sizeof(float));  // whole Tables struct in LDS
+static_assert(sizeof(Tables) % 16 == 0, "LDS regions after the tables stay 16-B aligned");
 
 struct StepArgs {
   State st;
@@ -52,14 +53,15 @@ struct StepArgs {
 
 // Generic: runtime (G, C, R), LIDAR offsets from the handle's table.
 __device__ __forceinline__ void build_obs_generic(const StepArgs& a, int64_t e, int x, int y, float* row,
-                                                  const float* tdist, const float* tpos, const float* tvis) {
+                                                  const float* tdist, const float* tpos, const float* tvis,
+                                                  const signed char* ldx, const signed char* ldy) {
   const Geo& g = a.g;
   const int R = g.R, C = g.C;
   for (int i = 0; i < C; ++i) {
     int dist = R, ent = EMPTY;
     for (int r = 1; r <= R; ++r) {
-      int cx = x + a.st.ldx[i * R + r - 1];
-      int cy = y + a.st.ldy[i * R + r - 1];
+      int cx = x + ldx[i * R + r - 1];
+      int cy = y + ldy[i * R + r - 1];
       int code = (cx >= 0 && cx < g.G) ? grid_code(a.st, g, e, cx, cy + R) : OBST;  // :271-284
       if (code != EMPTY) {
         dist = r;
@@ -80,6 +82,42 @@ __device__ __forceinline__ void build_obs_generic(const StepArgs& a, int64_t e, 
     uint32_t win = (xr >= 0 && xr < g.G) ? vis_window(a.st, g, e, xr, y) : 0xAAAAAu;
     for (int ly = 0; ly < 5; ++ly) row[5 * C + 2 + 5 * lx + ly] = tvis[(win >> (4 * ly)) & 15u];
   }
+}
+
+// obs of a freshly reset env (all visits 0 but the rover's 1) from its grid image
+// sg, written to `out` (HBM).  Same values as build_obs_generic on that state.
+__device__ inline void build_obs_fresh(const StepArgs& a, const uint64_t* sg, const Scal& s, float* out,
+                                       const float* tdist, const float* tpos, const float* tvis,
+                                       const signed char* ldx, const signed char* ldy) {
+  const Geo& g = a.g;
+  const int R = g.R, C = g.C, x = s.x, y = s.y;
+  for (int i = 0; i < C; ++i) {
+    int dist = R, ent = EMPTY;
+    for (int r = 1; r <= R; ++r) {
+      const int cx = x + ldx[i * R + r - 1];
+      const int cy = y + ldy[i * R + r - 1];
+      const int code = (cx >= 0 && cx < g.G) ? img_code(sg, g, cx, cy + R) : OBST;  // :271-284
+      if (code != EMPTY) {
+        dist = r;
+        ent = code;
+        break;
+      }
+    }
+    out[5 * i] = tdist[dist];
+    out[5 * i + 1] = ent == 0 ? 1.0f : 0.0f;
+    out[5 * i + 2] = ent == 1 ? 1.0f : 0.0f;
+    out[5 * i + 3] = ent == 2 ? 1.0f : 0.0f;
+    out[5 * i + 4] = ent == 3 ? 1.0f : 0.0f;
+  }
+  out[5 * C] = tpos[x];
+  out[5 * C + 1] = tpos[y];
+  for (int lx = 0; lx < 5; ++lx)
+    for (int ly = 0; ly < 5; ++ly) {
+      const int gx = x + lx - 2, gy = y + ly - 2;
+      const bool in = gx >= 0 && gx < g.G && gy >= 0 && gy < g.G;       // :307-311
+      const bool rover = lx == 2 && ly == 2 && !(s.flags & F_NOROOM);
+      out[5 * C + 2 + 5 * lx + ly] = !in ? tvis[10] : (rover ? tvis[1] : tvis[0]);
+    }
 }
 
 // ------------------------------------------------------------------ transition
@@ -182,6 +220,7 @@ __global__ __launch_bounds__(kBlock) void pe_step_kernel(StepArgs a) {
   float* tvis = smem + 328;
   float* rows = smem + kTabFloats;
   load_tables(smem, a.st.tab);
+  const Tables* ltab = reinterpret_cast<const Tables*>(smem);
   __syncthreads();
   const int64_t e0 = (int64_t)blockIdx.x * kBlock;
   const int64_t e = e0 + threadIdx.x;
@@ -199,19 +238,19 @@ __global__ __launch_bounds__(kBlock) void pe_step_kernel(StepArgs a) {
     if ((term || trunc) && a.autoreset) {
       // DummyVecEnv.step_wait: keep the terminal obs, reset, return the reset obs.
       if (a.tobs) {
-        build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis);
+        build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis, a.st.ldx, a.st.ldy);
         float* t = a.tobs + e * a.g.D;
         for (int k = 0; k < a.g.D; ++k) t[k] = row[k];
       }
       if (a.ep_ret_out) a.ep_ret_out[e] = ret;
       if (a.ep_len_out) a.ep_len_out[e] = s.step;
-      if (a.tinfo) write_info(a.st, a.g, e, s, a.tinfo + e * PE_NINFO);
-      s = reset_env(a.st, a.g, a.rl, e, s.episode);
+      if (a.tinfo) write_info(a.st, a.g, ltab, e, s, a.tinfo + e * PE_NINFO);
+      s = reset_env(a.st, a.g, a.rl, ltab, e, s.episode);
       ret = 0.0;
     }
     a.st.ep_ret[e] = ret;
     a.st.scal[e] = pack(s);
-    build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis);
+    build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis, a.st.ldx, a.st.ldy);
   }
   __syncthreads();
   const int64_t valid = a.n - e0 < kBlock ? a.n - e0 : kBlock;
@@ -245,6 +284,7 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
     ret = st.ep_ret[e];
   }
   load_tables(smem, st.tab);
+  const Tables* ltab = reinterpret_cast<const Tables*>(smem);
   __syncthreads();
   if (live) {
     Scal s = unpack(sw);
@@ -368,11 +408,11 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
       }
       if (a.ep_ret_out) a.ep_ret_out[e] = ret;
       if (a.ep_len_out) a.ep_len_out[e] = s.step;
-      if (a.tinfo) write_info(a.st, a.g, e, s, a.tinfo + e * PE_NINFO);
-      s = reset_env(st, g, rl, e, s.episode);
+      if (a.tinfo) write_info(a.st, a.g, ltab, e, s, a.tinfo + e * PE_NINFO);
+      s = reset_env(st, g, rl, ltab, e, s.episode);
       st.ep_ret[e] = 0.0;
       st.scal[e] = pack(s);
-      build_obs_generic(a, e, s.x, s.y, row, smem, tpos, tvis);  // fresh map: rare path
+      build_obs_generic(a, e, s.x, s.y, row, smem, tpos, tvis, a.st.ldx, a.st.ldy);  // fresh map: rare path
     } else {
       st.ep_ret[e] = ret;
       st.scal[e] = pack(s);
@@ -396,9 +436,9 @@ constexpr int kAblate = 0;
 // Diagnostic phase stamps (tools/stamps.py builds a SEPARATE library with
 // -DPE_STAMPS): lane 0 of every wave of the sector kernel records s_memrealtime
 // (100 MHz) at 8 points; pe_debug_stamps() copies them out.  Not in the product build.
-#ifdef PE_STAMPS
+#if defined(PE_STAMPS) || defined(PE_STAMPS_RESET)
 __device__ uint64_t g_stamps[16384 * 8];
-#define PE_STAMP(k)                                                                         \
+#define PE_STAMP_RAW(k)                                                                     \
   do {                                                                                      \
     uint64_t _t;                                                                            \
     __builtin_amdgcn_sched_barrier(0);                                                      \
@@ -407,9 +447,19 @@ __device__ uint64_t g_stamps[16384 * 8];
     const int _w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);                     \
     if ((threadIdx.x & 63) == 0 && _w < 16384) g_stamps[_w * 8 + (k)] = _t;                \
   } while (0)
+#endif
+#ifdef PE_STAMPS
+#define PE_STAMP(k) PE_STAMP_RAW(k)
 #else
 #define PE_STAMP(k) \
   do {              \
+  } while (0)
+#endif
+#ifdef PE_STAMPS_RESET
+#define PE_RSTAMP(k) PE_STAMP_RAW(k)
+#else
+#define PE_RSTAMP(k) \
+  do {               \
   } while (0)
 #endif
 
@@ -421,7 +471,7 @@ constexpr int quad_tile_off() {
 }
 
 template <int C, int R, bool ONEWORD, int NW>
-__global__ __launch_bounds__(64 * NW) void pe_step_quad(StepArgs a) {
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs
   constexpr int NR = 2 * R + 3, NV = 7, EPB = kQuadEnvs, CW = NW - 1;  // CW: commit wave
   static_assert(C % NW == 0, "rays must split evenly over the waves");
   static_assert(ONEWORD || R <= 14, "funnel-shifted window row must hold 2R+5 cells");
@@ -460,6 +510,7 @@ __global__ __launch_bounds__(64 * NW) void pe_step_quad(StepArgs a) {
   }
   if (llive) lw = st.scal[el];
   load_tables(smem, st.tab);
+  const Tables* ltab = reinterpret_cast<const Tables*>(smem);
   Scal s = unpack(sw);
 #ifdef PE_STAMPS
   if ((int)(s.x + lw.x) == -12345) g_stamps[0] = 1;  // consume round 1 before the stamp
@@ -618,8 +669,10 @@ __global__ __launch_bounds__(64 * NW) void pe_step_quad(StepArgs a) {
     const int sh = 2 * (yp - yb);
     const int vs = 4 * (yp - ybv);
     if constexpr (!(kAblate & 2)) sector_rays<C, R, NW>(wv, lrow, lane, kc, sh, watered, row);
-    for (int lx = wv; lx < 5; lx += NW) quad_slice_row(lvis, lane, lx, dxv, vs, ok, nib, C, row, tvis);
-    if (wv == (NW == 4 ? 1 : 5)) {
+    // slice rows and position go to the non-commit waves (the commit wave is the laggard)
+    if (wv != CW)
+      for (int lx = wv; lx < 5; lx += NW - 1) quad_slice_row(lvis, lane, lx, dxv, vs, ok, nib, C, row, tvis);
+    if (wv == (NW == 4 ? 2 : 5)) {
       row[5 * C] = tpos[xp];                                      // :294-296
       row[5 * C + 1] = tpos[yp];
     }
@@ -685,7 +738,25 @@ __global__ __launch_bounds__(64 * NW) void pe_step_quad(StepArgs a) {
   // ---- DummyVecEnv auto-reset (rare): commit wave, after the whole obs row is in LDS
   const int any_done = __syncthreads_or(done);
   PE_STAMP(5);
+  // The done env's own obs-tile row is free once its terminal obs is copied out:
+  // when it can hold the grid image, the new map is generated there (LDS latency
+  // for the rejection-sampling scans) and the fresh obs row goes straight to HBM
+  // after the tile store.
+  const bool scratch_ok = reset_scratch_bytes(g.G, g.WPR, rl.P) <= 4 * g.D;
+  // 8-B aligned start inside the row (rows is 16-B aligned, D is odd); pointer
+  // arithmetic keeps the LDS address space visible to the compiler (ds_* ops)
+  uint64_t* sg = reinterpret_cast<uint64_t*>(row + ((lane * g.D) & 1));
+  // LIDAR offsets for the reset-path obs builders, staged in the (now dead) window region
+  static_assert(2 * C * R <= (NR * 8 + NV * 4) * EPB, "offset tables must fit the window region");
+  const signed char* lldx = reinterpret_cast<const signed char*>(lrow);
+  const signed char* lldy = lldx + C * R;
   if (any_done) {
+    PE_RSTAMP(0);
+    for (int k = threadIdx.x; k < C * R; k += blockDim.x) {
+      reinterpret_cast<signed char*>(lrow)[k] = st.ldx[k];
+      reinterpret_cast<signed char*>(lrow)[C * R + k] = st.ldy[k];
+    }
+    __syncthreads();
     if (done) {
       if (a.tobs) {
         float* t = a.tobs + e * g.D;
@@ -693,16 +764,32 @@ __global__ __launch_bounds__(64 * NW) void pe_step_quad(StepArgs a) {
       }
       if (a.ep_ret_out) a.ep_ret_out[e] = ret;
       if (a.ep_len_out) a.ep_len_out[e] = s.step;
-      if (a.tinfo) write_info(a.st, a.g, e, s, a.tinfo + e * PE_NINFO);
-      s = reset_env(st, g, rl, e, s.episode);
+      PE_RSTAMP(1);
+      if (a.tinfo) write_info(a.st, a.g, ltab, e, s, a.tinfo + e * PE_NINFO);
+      PE_RSTAMP(2);
+      if (scratch_ok) {
+        s = reset_env_scratch(st, g, rl, ltab, e, s.episode, sg);
+        PE_RSTAMP(3);
+      } else {
+        s = reset_env(st, g, rl, ltab, e, s.episode);
+        build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis, lldx, lldy);
+      }
       st.ep_ret[e] = 0.0;
       st.scal[e] = pack(s);
-      build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis);
     }
     __syncthreads();
   }
   const int64_t valid = a.n - e0 < EPB ? a.n - e0 : EPB;
   if constexpr (!(kAblate & 1)) store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D);
+  if (any_done && scratch_ok) {
+    // the tile store above wrote scratch bytes into the done rows: drain it, then
+    // overwrite those rows with the fresh obs built from the LDS grid image
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    PE_RSTAMP(4);
+    if (done) build_obs_fresh(a, sg, s, a.obs + e * g.D, tdist, tpos, tvis, lldx, lldy);
+    PE_RSTAMP(5);
+  }
   PE_STAMP(6);
 #ifdef PE_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -717,24 +804,45 @@ __global__ __launch_bounds__(kBlock) void pe_reset_kernel(StepArgs a) {
   float* tpos = smem + 72;
   float* tvis = smem + 328;
   float* rows = smem + kTabFloats;
+  const Geo& g = a.g;
+  // LIDAR offsets after the tile (read by the obs builders in dependent chains)
+  signed char* lldx = reinterpret_cast<signed char*>(rows + kBlock * g.DS);
+  signed char* lldy = lldx + g.C * g.R;
   load_tables(smem, a.st.tab);
+  for (int k = threadIdx.x; k < g.C * g.R; k += blockDim.x) {
+    lldx[k] = a.st.ldx[k];
+    lldy[k] = a.st.ldy[k];
+  }
+  const Tables* ltab = reinterpret_cast<const Tables*>(smem);
   __syncthreads();
   const int64_t e0 = (int64_t)blockIdx.x * kBlock;
   const int64_t e = e0 + threadIdx.x;
-  float* row = rows + threadIdx.x * a.g.DS;
+  float* row = rows + threadIdx.x * g.DS;
+  // a resetting env generates its map in its own tile row (LDS), cf. pe_step_quad
+  const bool scratch_ok = reset_scratch_bytes(g.G, g.WPR, a.rl.P) <= 4 * g.DS;
+  uint64_t* sg = reinterpret_cast<uint64_t*>(row + ((threadIdx.x * g.DS) & 1));
+  bool resetting = false;
+  Scal s;
   if (e < a.n) {
-    Scal s = unpack(a.st.scal[e]);
-    if (!a.mask || a.mask[e]) {
-      s = reset_env(a.st, a.g, a.rl, e, s.episode);
+    s = unpack(a.st.scal[e]);
+    resetting = !a.mask || a.mask[e];
+    if (resetting) {
+      s = scratch_ok ? reset_env_scratch(a.st, g, a.rl, ltab, e, s.episode, sg)
+                     : reset_env(a.st, g, a.rl, ltab, e, s.episode);
       a.st.ep_ret[e] = 0.0;
       a.st.scal[e] = pack(s);
     }
-    if (a.obs) build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis);
+    if (a.obs && !(resetting && scratch_ok)) build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis, lldx, lldy);
   }
   if (!a.obs) return;
   __syncthreads();
   const int64_t valid = a.n - e0 < kBlock ? a.n - e0 : kBlock;
-  store_tile(rows, a.obs + e0 * a.g.D, (int)valid, a.g.D, a.g.DS);
+  store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.DS);
+  if (scratch_ok) {  // overwrite the scratch rows the tile store wrote
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (resetting) build_obs_fresh(a, sg, s, a.obs + e * g.D, tdist, tpos, tvis, lldx, lldy);
+  }
 }
 
 // pe_load_maps: host-supplied layouts (CPython-stream reset mode).
@@ -746,6 +854,7 @@ __global__ __launch_bounds__(kBlock) void pe_load_maps_kernel(StepArgs a, int k,
   float* tvis = smem + 328;
   float* rows = smem + kTabFloats;
   load_tables(smem, a.st.tab);
+  const Tables* ltab = reinterpret_cast<const Tables*>(smem);
   __syncthreads();
   const int j = blockIdx.x * kBlock + threadIdx.x;
   if (j >= k) return;
@@ -775,7 +884,7 @@ __global__ __launch_bounds__(kBlock) void pe_load_maps_kernel(StepArgs a, int k,
   a.st.scal[e] = pack(s);
   a.st.ep_ret[e] = 0.0;
   float* row = rows + threadIdx.x * g.DS;
-  build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis);
+  build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis, a.st.ldx, a.st.ldy);
   if (a.obs)
     for (int q = 0; q < g.D; ++q) a.obs[(int64_t)j * g.D + q] = row[q];
 }
@@ -786,7 +895,7 @@ __global__ void pe_info_kernel(StepArgs a, int32_t* info) {
   if (e >= a.n) return;
   const Geo& g = a.g;
   static_assert(PE_NINFO == 11 && PE_I_POISONED == 10, "write_info column layout");
-  write_info(a.st, g, e, unpack(a.st.scal[e]), info + e * PE_NINFO);
+  write_info(a.st, g, a.st.tab, e, unpack(a.st.scal[e]), info + e * PE_NINFO);
 }
 
 // get_state: one thread per (env, cell).
@@ -989,7 +1098,9 @@ StepArgs base_args(const pe_handle* h) {
   return a;
 }
 
-size_t lds_bytes(const Geo& g) { return sizeof(float) * (size_t)(kTabFloats + kBlock * g.DS); }
+size_t lds_bytes(const Geo& g) {
+  return sizeof(float) * (size_t)(kTabFloats + kBlock * g.DS) + align_up(2 * (size_t)g.C * g.R, 16);
+}
 
 // Step kernel variants.  The quadrant kernels (4 waves x 64 envs per workgroup)
 // are the default for the specialized geometries; the one-lane-per-env kernels
@@ -1409,7 +1520,7 @@ int pe_poll_errors(pe_handle* h, int32_t* bits, void* stream) {
   return PE_OK;
 }
 
-#ifdef PE_STAMPS
+#if defined(PE_STAMPS) || defined(PE_STAMPS_RESET)
 int pe_debug_stamps(uint64_t* host, int64_t count) {
   if (count > 16384 * 8) count = 16384 * 8;
   PE_HIP(hipDeviceSynchronize());

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Time the all-env auto-reset step (step 1000 of a synchronized batch) vs a plain step."""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "rl-env_amd"))
+import torch  # noqa: E402
+
+from plantos_amd import PlantOSBatch  # noqa: E402
+
+
+def main():
+    G = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    C = 16 if G <= 32 else 64
+    P, O = (10, 12) if G <= 32 else (100, 120)
+    n = 65536
+    b = PlantOSBatch(n, grid_size=G, num_plants=P, num_obstacles=O, lidar_range=6, lidar_channels=C, device="cuda:0")
+    acts = torch.empty((64, n), dtype=torch.int32, device="cuda:0")
+    for t in range(64):
+        b.synth_actions(0, t, out=acts[t])
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    for t in range(998):
+        b.step(acts[t % 64])
+    torch.cuda.synchronize()
+    ev[0].record()
+    b.step(acts[998 % 64])
+    ev[1].record()
+    b.step(acts[999 % 64])  # step 1000: every env truncates and resets
+    ev[2].record()
+    torch.cuda.synchronize()
+    tr = b.truncated.float().mean().item()
+    t0 = torch.cuda.Event(enable_timing=True)
+    t1 = torch.cuda.Event(enable_timing=True)
+    t0.record()
+    b.reset()
+    t1.record()
+    torch.cuda.synchronize()
+    print(json.dumps({"kernel": b.kernel_name, "grid": G, "plain_step_ms": ev[0].elapsed_time(ev[1]),
+                      "reset_step_ms": ev[1].elapsed_time(ev[2]), "truncated_frac": tr,
+                      "pe_reset_all_ms": t0.elapsed_time(t1)}))
+
+
+if __name__ == "__main__":
+    main()
