@@ -191,6 +191,22 @@ __device__ __forceinline__ void load_tables(float* smem, const Tables* tab) {
   for (int k = threadIdx.x; k < kTabFloats; k += blockDim.x) smem[k] = src[k];
 }
 
+// Only the tables the step's hot path reads: dist[0..R], pos[0..G), vis[0..16).
+__device__ __forceinline__ void load_tables_hot(float* smem, const Tables* tab, int G, int R) {
+  const float* src = reinterpret_cast<const float*>(tab);
+  const int n = (R + 1) + G + 16;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    const int f = k <= R ? k : (k < R + 1 + G ? 72 + (k - R - 1) : 328 + (k - R - 1 - G));
+    smem[f] = src[f];
+  }
+}
+
+// The rest (pad masks, read by map generation / info): loaded on the rare reset path.
+__device__ __forceinline__ void load_tables_cold(float* smem, const Tables* tab) {
+  const float* src = reinterpret_cast<const float*>(tab);
+  for (int k = 344 + (int)threadIdx.x; k < kTabFloats; k += blockDim.x) smem[k] = src[k];
+}
+
 // Stream the block's [valid x D] obs tile (LDS rows of stride DS) to HBM.
 __device__ __forceinline__ void store_tile(const float* rows, float* dst, int valid, int D, int DS) {
   const int total = valid * D;
@@ -426,7 +442,9 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
 
 // Diagnostic phase ablation (tools/ablate.py builds a SEPARATE library with
 // -DPE_ABLATE=bits; the product library is built without it): 1 = no obs tile
-// store, 2 = no ray-march, 4 = no round-2 window loads, 8 = no state commit.
+// store, 2 = no ray-march, 4 = no round-2 window loads, 8 = no state commit,
+// 16 = no visit-row loads, 32 = no grid-row loads, 64 = timing probe: the block's
+// whole grid + visit blocks streamed in round 1 (coalesced) instead of round 2.
 #ifdef PE_ABLATE
 constexpr int kAblate = PE_ABLATE;
 #else
@@ -509,7 +527,16 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
     if (wv == CW) ret = st.ep_ret[e];
   }
   if (llive) lw = st.scal[el];
-  load_tables(smem, st.tab);
+  if constexpr ((kAblate & 64) != 0) {  // diagnostic only: whole-block streaming probe
+    const uint4* gsrc = reinterpret_cast<const uint4*>(st.grid + e0 * g.gstride);
+    const uint4* vsrc = reinterpret_cast<const uint4*>(st.vis + e0 * g.vstride);
+    const int ng = (int)(EPB * g.gstride / 2), nv = (int)(EPB * g.vstride / 4);
+    uint32_t acc = 0;
+    for (int k = threadIdx.x; k < ng; k += blockDim.x) acc ^= gsrc[k].x ^ gsrc[k].w;
+    for (int k = threadIdx.x; k < nv; k += blockDim.x) acc ^= vsrc[k].y ^ vsrc[k].z;
+    reinterpret_cast<uint32_t*>(smem + quad_tile_off<R>())[threadIdx.x] = acc;
+  }
+  load_tables_hot(smem, st.tab, a.g.G, R);
   const Tables* ltab = reinterpret_cast<const Tables*>(smem);
   Scal s = unpack(sw);
 #ifdef PE_STAMPS
@@ -553,7 +580,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
 #pragma unroll
       for (int j = 0; j < (NP + LT - 1) / LT; ++j) {
         const int pp = sub + LT * j;
-        if (pp < NP) {
+        if (pp < NP && !(kAblate & 32)) {
           const int ra = ps + 2 * pp;
           uint64_t va = kEven64, vb2 = kEven64;  // off-map rows: obstacles
           if (ra >= 0 && ra + 1 < g.G) {
@@ -575,7 +602,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
 #pragma unroll
       for (int j = 0; j < (NV + LT - 1) / LT; ++j) {
         const int k = sub + LT * j;
-        if (k < NV) {
+        if (k < NV && !(kAblate & 16)) {
           const int xr = lx - 3 + k;
           uint32_t lo = 0xAAAAAAAAu, hi = 0xAAAAAAAAu;  // off-map row: visit 10 (reads 1.0)
           if (xr >= 0 && xr < g.G) {
@@ -752,6 +779,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
   const signed char* lldy = lldx + C * R;
   if (any_done) {
     PE_RSTAMP(0);
+    load_tables_cold(smem, st.tab);
     for (int k = threadIdx.x; k < C * R; k += blockDim.x) {
       reinterpret_cast<signed char*>(lrow)[k] = st.ldx[k];
       reinterpret_cast<signed char*>(lrow)[C * R + k] = st.ldy[k];

@@ -21,12 +21,13 @@ SO = os.path.join(REPO, "build", "stamps", "libplantos_hip_stamps.so")
 NAMES = ["entry", "round1", "round2+lds", "barrier", "compute", "barrier_or", "store_issue", "store_drain"]
 
 
-def build():
-    os.makedirs(os.path.dirname(SO), exist_ok=True)
+def build(ablate=0):
+    so = SO if not ablate else SO.replace(".so", f"_abl{ablate}.so")
+    os.makedirs(os.path.dirname(so), exist_ok=True)
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                    "-DPE_STAMPS", "-o", SO, os.path.join(REPO, "rl-env_amd", "csrc", "plantos_batch.hip")],
-                   check=True)
-    print(SO)
+                    "-DPE_STAMPS", f"-DPE_ABLATE={ablate}", "-o", so,
+                    os.path.join(REPO, "rl-env_amd", "csrc", "plantos_batch.hip")], check=True)
+    print(so)
 
 
 def pct(v, q):
@@ -35,7 +36,8 @@ def pct(v, q):
 
 
 def run(argv):
-    os.environ["PLANTOS_HIP_LIB"] = SO
+    abl = int(argv[argv.index("--ablate") + 1]) if "--ablate" in argv else 0
+    os.environ["PLANTOS_HIP_LIB"] = SO if not abl else SO.replace(".so", f"_abl{abl}.so")
     sys.path.insert(0, os.path.join(REPO, "rl-env_amd"))
     import numpy as np
     import torch
@@ -77,6 +79,6 @@ def run(argv):
 
 if __name__ == "__main__":
     if sys.argv[1] == "build":
-        build()
+        build(int(sys.argv[2]) if len(sys.argv) > 2 else 0)
     else:
         run(sys.argv[2:])
