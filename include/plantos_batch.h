@@ -152,6 +152,21 @@ int pe_synth_actions(pe_handle* h, uint64_t seed, uint32_t t, int32_t* actions, 
  * layout); synchronizes the stream. */
 int pe_poll_errors(pe_handle* h, int32_t* bits, void* stream);
 
+/* Seed-exact reset layouts (host side): the reference's _generate_map
+ * (plantos_env.py:338-372) on CPython's global `random` stream after
+ * random.seed(seed), including CPython 3.10 set iteration order, so the maps are
+ * the ones the reference produces.  Maps come out in stream order; a DummyVecEnv
+ * consumes them in env-index order at reset() and then per step (done envs in
+ * index order).  Feed them to pe_load_maps.  pe_pystream_next fails with
+ * PE_ERR_NOROOM where the reference raises ValueError (360-364). */
+typedef struct pe_pystream pe_pystream;
+int pe_pystream_create(const pe_config* c, int64_t seed, pe_pystream** out);
+/* next k maps: cells u8[k,G,G] (pe_cell codes), rover i32[k,2]; HOST pointers */
+int pe_pystream_next(pe_pystream* s, int32_t k, uint8_t* cells, int32_t* rover);
+/* random.getrandbits(32) on the stream (tests pin the number of draws consumed) */
+uint32_t pe_pystream_getrandbits32(pe_pystream* s);
+int pe_pystream_destroy(pe_pystream* s);
+
 /* Introspection for tests / benchmarks. */
 int32_t pe_num_envs(const pe_handle* h);
 int32_t pe_kernel_variant(const pe_handle* h);  /* 0 generic, >0 specialized geometry */

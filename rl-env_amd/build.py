@@ -11,7 +11,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "plantos_batch.hip")
-DEPS = [SRC, os.path.join(HERE, "csrc", "pe_device.hpp"), os.path.join(HERE, "csrc", "pe_fast.hpp"), os.path.join(REPO, "include", "plantos_batch.h"),
+SRC_HOST = os.path.join(HERE, "csrc", "pe_pystream.cpp")
+DEPS = [SRC, SRC_HOST, os.path.join(HERE, "csrc", "pe_device.hpp"), os.path.join(HERE, "csrc", "pe_fast.hpp"), os.path.join(REPO, "include", "plantos_batch.h"),
         os.path.join(HERE, "tools_gen_lidar.py")]
 OUT = os.path.join(HERE, "plantos_amd", "libplantos_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -24,7 +25,7 @@ def build(force=False, verbose=False):
     deps = DEPS + [os.path.join(HERE, "csrc", "lidar_tables.inc")]
     if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= max(os.path.getmtime(d) for d in deps):
         return OUT
-    cmd = [HIPCC] + FLAGS + ["-o", OUT, SRC]
+    cmd = [HIPCC] + FLAGS + ["-o", OUT, SRC, SRC_HOST]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

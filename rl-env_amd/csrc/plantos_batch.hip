@@ -251,8 +251,9 @@ __global__ __launch_bounds__(kBlock) void pe_step_kernel(StepArgs a) {
     a.reward[e] = (float)rew;
     a.term[e] = term;
     a.trunc[e] = trunc;
-    if ((term || trunc) && a.autoreset) {
-      // DummyVecEnv.step_wait: keep the terminal obs, reset, return the reset obs.
+    if (term || trunc) {
+      // terminal outputs of an ended episode; DummyVecEnv.step_wait then resets
+      // and returns the reset obs (autoreset), else the caller resets (pe_load_maps)
       if (a.tobs) {
         build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis, a.st.ldx, a.st.ldy);
         float* t = a.tobs + e * a.g.D;
@@ -261,8 +262,10 @@ __global__ __launch_bounds__(kBlock) void pe_step_kernel(StepArgs a) {
       if (a.ep_ret_out) a.ep_ret_out[e] = ret;
       if (a.ep_len_out) a.ep_len_out[e] = s.step;
       if (a.tinfo) write_info(a.st, a.g, ltab, e, s, a.tinfo + e * PE_NINFO);
-      s = reset_env(a.st, a.g, a.rl, ltab, e, s.episode);
-      ret = 0.0;
+      if (a.autoreset) {
+        s = reset_env(a.st, a.g, a.rl, ltab, e, s.episode);
+        ret = 0.0;
+      }
     }
     a.st.ep_ret[e] = ret;
     a.st.scal[e] = pack(s);
@@ -416,7 +419,7 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
     a.reward[e] = (float)rew;
     a.term[e] = term;
     a.trunc[e] = trunc;
-    if ((term || trunc) && a.autoreset) {                          // DummyVecEnv auto-reset
+    if (term || trunc) {                                           // ended: terminal outputs
       if (a.tobs) {
         obs_from_window<C, R, ONEWORD>(w, g.G, dxv, s.x, s.y, row, tpos, tvis);
         float* t = a.tobs + e * g.D;
@@ -425,6 +428,8 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
       if (a.ep_ret_out) a.ep_ret_out[e] = ret;
       if (a.ep_len_out) a.ep_len_out[e] = s.step;
       if (a.tinfo) write_info(a.st, a.g, ltab, e, s, a.tinfo + e * PE_NINFO);
+    }
+    if ((term || trunc) && a.autoreset) {                          // DummyVecEnv auto-reset
       s = reset_env(st, g, rl, ltab, e, s.episode);
       st.ep_ret[e] = 0.0;
       st.scal[e] = pack(s);
@@ -758,7 +763,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
       a.trunc[e] = trunc;
       st.ep_ret[e] = ret;
       st.scal[e] = pack(s);
-      done = (term || trunc) && a.autoreset;
+      done = term || trunc;  // terminal outputs; the reset itself only with autoreset
     }
   }
   PE_STAMP(4);
@@ -795,21 +800,24 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
       PE_RSTAMP(1);
       if (a.tinfo) write_info(a.st, a.g, ltab, e, s, a.tinfo + e * PE_NINFO);
       PE_RSTAMP(2);
-      if (scratch_ok) {
+      if (!a.autoreset) {
+      } else if (scratch_ok) {
         s = reset_env_scratch(st, g, rl, ltab, e, s.episode, sg);
         PE_RSTAMP(3);
       } else {
         s = reset_env(st, g, rl, ltab, e, s.episode);
         build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis, lldx, lldy);
       }
-      st.ep_ret[e] = 0.0;
-      st.scal[e] = pack(s);
+      if (a.autoreset) {
+        st.ep_ret[e] = 0.0;
+        st.scal[e] = pack(s);
+      }
     }
     __syncthreads();
   }
   const int64_t valid = a.n - e0 < EPB ? a.n - e0 : EPB;
   if constexpr (!(kAblate & 1)) store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D);
-  if (any_done && scratch_ok) {
+  if (any_done && scratch_ok && a.autoreset) {
     // the tile store above wrote scratch bytes into the done rows: drain it, then
     // overwrite those rows with the fresh obs built from the LDS grid image
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1234,6 +1242,8 @@ void pe_default_config(pe_config* c, int32_t G, int32_t P, int32_t O, int32_t R,
 int32_t pe_obs_dim(const pe_config* c) { return c->lidar_channels * 5 + 2 + 25; }
 
 const char* pe_last_error(void) { return g_err.c_str(); }
+
+int pe_internal_set_error(int code, const char* msg) { return fail(code, msg); }
 
 int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** out) {
   if (!c || !out) return fail(PE_ERR_ARG, "null argument");

@@ -29,6 +29,7 @@ EXPORTS = [
     "pe_default_config", "pe_obs_dim", "pe_create", "pe_destroy", "pe_seed", "pe_reset", "pe_step",
     "pe_get_info", "pe_get_state", "pe_set_state", "pe_load_maps", "pe_synth_actions", "pe_poll_errors",
     "pe_num_envs", "pe_kernel_variant", "pe_kernel_name", "pe_state_bytes", "pe_last_error",
+    "pe_pystream_create", "pe_pystream_next", "pe_pystream_getrandbits32", "pe_pystream_destroy",
 ]
 
 
@@ -88,8 +89,14 @@ def lib():
     L.pe_state_bytes.restype = U64
     L.pe_last_error.argtypes = []
     L.pe_last_error.restype = ctypes.c_char_p
+    L.pe_pystream_create.argtypes = [CP, ctypes.c_int64, ctypes.POINTER(P)]
+    L.pe_pystream_next.argtypes = [P, I32, P, P]
+    L.pe_pystream_getrandbits32.argtypes = [P]
+    L.pe_pystream_getrandbits32.restype = U32
+    L.pe_pystream_destroy.argtypes = [P]
     for name in ("pe_create", "pe_destroy", "pe_seed", "pe_reset", "pe_step", "pe_get_info", "pe_get_state",
-                 "pe_set_state", "pe_load_maps", "pe_synth_actions", "pe_poll_errors"):
+                 "pe_set_state", "pe_load_maps", "pe_synth_actions", "pe_poll_errors", "pe_pystream_create",
+                 "pe_pystream_next", "pe_pystream_destroy"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
@@ -109,3 +116,41 @@ def default_config(grid_size, num_plants, num_obstacles, lidar_range, lidar_chan
     c = PEConfig()
     lib().pe_default_config(ctypes.byref(c), grid_size, num_plants, num_obstacles, lidar_range, lidar_channels)
     return c
+
+
+class PyStream:
+    """Host-side CPython `random` map stream (seed-exact reset layouts,
+    plantos_env.py:338-372 after random.seed(seed)); see include/plantos_batch.h."""
+
+    def __init__(self, grid_size, num_plants, num_obstacles, seed, thirsty_plant_prob=0.7):
+        import numpy as np
+        self._np = np
+        self.G = grid_size
+        c = default_config(grid_size, num_plants, num_obstacles, 1, 1)
+        c.thirsty_plant_prob = float(thirsty_plant_prob)
+        h = ctypes.c_void_p()
+        check(lib().pe_pystream_create(ctypes.byref(c), int(seed), ctypes.byref(h)), "pe_pystream_create")
+        self._h = h
+
+    def next(self, k):
+        """next k maps in stream order: cells u8[k,G,G], rover i32[k,2] (numpy)."""
+        np = self._np
+        cells = np.zeros((k, self.G, self.G), np.uint8)
+        rover = np.zeros((k, 2), np.int32)
+        check(lib().pe_pystream_next(self._h, int(k), cells.ctypes.data_as(ctypes.c_void_p),
+                                     rover.ctypes.data_as(ctypes.c_void_p)), "pe_pystream_next")
+        return cells, rover
+
+    def getrandbits32(self):
+        return int(lib().pe_pystream_getrandbits32(self._h))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().pe_pystream_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass

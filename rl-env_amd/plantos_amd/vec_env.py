@@ -149,14 +149,26 @@ class _StepView:
         self._len = None
         self._done_idx = np.nonzero(done_np)[0]
         self._t = round(time.time() - venv._t_start, 6)
+        self._expired = False
+
+    def expire(self):
+        """The next step overwrites the device buffers this view reads lazily."""
+        self._expired = True
+
+    def _check(self):
+        if self._expired:
+            raise RuntimeError("infos of a previous step must be read before the next step() "
+                               "(they are built lazily from device buffers)")
 
     def table(self):
         if self._info is None:
+            self._check()
             self._info = self.v.batch.get_info().cpu().numpy()
         return self._info
 
     def _terminal(self):
         if self._tinfo is None:
+            self._check()
             b = self.v.batch
             idx = torch.as_tensor(self._done_idx, device=b.device)
             self._tinfo = b.terminal_info.index_select(0, idx).cpu().numpy()
@@ -188,13 +200,25 @@ class PlantOSVecEnv(_VecEnvBase):
 
     def __init__(self, num_envs, grid_size=21, num_plants=8, num_obstacles=50, lidar_range=2, lidar_channels=10,
                  thirsty_plant_prob=0.7, max_steps=1000, seed=0, device=None, tensors=False, env_id_offset=0,
-                 observation_mode="lidar", render_mode=None, batch=None):
+                 observation_mode="lidar", render_mode=None, batch=None, reset_mode="device", python_seed=None):
+        """reset_mode="device": maps from the device generator keyed by (seed, env id,
+        episode) -- the throughput mode.  reset_mode="cpython": the reference's own
+        layouts, seed-exact: CPython's global `random` after random.seed(python_seed)
+        (default: seed), consumed in DummyVecEnv order (pe_pystream, host side)."""
         if observation_mode != "lidar":
             raise ValueError("only observation_mode='lidar' exists in the reference (plantos_env.py:27)")
+        if reset_mode not in ("device", "cpython"):
+            raise ValueError("reset_mode must be 'device' or 'cpython'")
+        self.reset_mode = reset_mode
         self.batch = batch if batch is not None else PlantOSBatch(
             num_envs, grid_size=grid_size, num_plants=num_plants, num_obstacles=num_obstacles,
             lidar_range=lidar_range, lidar_channels=lidar_channels, thirsty_plant_prob=thirsty_plant_prob,
-            max_steps=max_steps, autoreset=True, seed=seed, env_id_offset=env_id_offset, device=device)
+            max_steps=max_steps, autoreset=reset_mode == "device", seed=seed, env_id_offset=env_id_offset,
+            device=device)
+        self._pystream = None
+        if reset_mode == "cpython":
+            self._pystream = C.PyStream(grid_size, num_plants, num_obstacles,
+                                        seed if python_seed is None else python_seed, thirsty_plant_prob)
         self.grid_size, self.num_plants, self.num_obstacles = grid_size, num_plants, num_obstacles
         self.lidar_range, self.lidar_channels = lidar_range, lidar_channels
         self.thirsty_plant_prob, self.max_steps = thirsty_plant_prob, max_steps
@@ -206,6 +230,7 @@ class PlantOSVecEnv(_VecEnvBase):
         self.num_envs = int(num_envs)
         self.observation_space, self.action_space = obs_space, act_space
         self.reset_infos = [{} for _ in range(self.num_envs)]
+        self._last_view = None
         self._actions = None
         self._t_start = time.time()
         self._seed = seed
@@ -215,12 +240,29 @@ class PlantOSVecEnv(_VecEnvBase):
         return t if self.tensors else t.cpu().numpy()
 
     # ------------------------------------------------------------------ VecEnv API
+    def _load_stream_maps(self, idx):
+        """Next len(idx) CPython-stream maps into envs idx (ascending), obs rows updated."""
+        cells, rover = self._pystream.next(len(idx))
+        fresh = self.batch.load_maps(idx, cells, rover)
+        self.batch.obs[torch.as_tensor(idx, device=self.batch.device)] = fresh
+
+    def _new_view(self, done_np, te_np, tr_np):
+        if self._last_view is not None:
+            self._last_view.expire()
+        self._last_view = _StepView(self, done_np, te_np, tr_np)
+        return self._last_view
+
     def reset(self):
         """All envs get a fresh map; returns obs [N, D]."""
-        obs = self.batch.reset()
-        view = _StepView(self, np.zeros(self.num_envs, bool), np.zeros(self.num_envs, bool),
-                         np.zeros(self.num_envs, bool))
-        self.reset_infos = LazyInfos(self.num_envs, view)
+        if self._last_view is not None:
+            self._last_view.expire()
+        if self.reset_mode == "cpython":
+            self._load_stream_maps(np.arange(self.num_envs))
+            obs = self.batch.obs
+        else:
+            obs = self.batch.reset()
+        z = np.zeros(self.num_envs, bool)
+        self.reset_infos = LazyInfos(self.num_envs, self._new_view(z, z, z))
         return self._out(obs.clone() if self.tensors else obs)
 
     def step_async(self, actions):
@@ -230,11 +272,17 @@ class PlantOSVecEnv(_VecEnvBase):
         if self._actions is None:
             raise RuntimeError("step_wait() without step_async()")
         a = self._actions
+        if self._last_view is not None:
+            self._last_view.expire()
         if isinstance(a, np.ndarray) or not isinstance(a, torch.Tensor):
             a = torch.as_tensor(np.asarray(a).reshape(-1).astype(np.int64), device=self.batch.device)
         obs, rew, te, tr = self.batch.step(a.reshape(-1))
         self._actions = None
         done = te.bool() | tr.bool()
+        if self.reset_mode == "cpython":  # DummyVecEnv: done envs reset in index order
+            idx = torch.nonzero(done).reshape(-1).cpu().numpy()
+            if len(idx):
+                self._load_stream_maps(idx)
         if self.tensors:
             done_np, te_np, tr_np = (x.cpu().numpy() for x in (done, te.bool(), tr.bool()))
             out = (obs.clone(), rew.clone(), done)
@@ -242,7 +290,7 @@ class PlantOSVecEnv(_VecEnvBase):
             obs_np, rew_np = obs.cpu().numpy(), rew.cpu().numpy()
             done_np, te_np, tr_np = done.cpu().numpy(), te.cpu().numpy().astype(bool), tr.cpu().numpy().astype(bool)
             out = (obs_np, rew_np, done_np)
-        infos = LazyInfos(self.num_envs, _StepView(self, done_np, te_np, tr_np))
+        infos = LazyInfos(self.num_envs, self._new_view(done_np, te_np, tr_np))
         return out[0], out[1], out[2], infos
 
     def step(self, actions):
@@ -251,6 +299,8 @@ class PlantOSVecEnv(_VecEnvBase):
 
     def close(self):
         self.batch.close()
+        if self._pystream is not None:
+            self._pystream.close()
 
     def seed(self, seed=None):
         """Re-key the device map generator; per-env seeds seed+i like DummyVecEnv."""
@@ -258,6 +308,10 @@ class PlantOSVecEnv(_VecEnvBase):
             seed = int(np.random.randint(0, 2 ** 31 - 1))
         self._seed = int(seed)
         self.batch.seed(int(seed))
+        if self.reset_mode == "cpython":  # random.seed(seed) of the reference's global stream
+            self._pystream.close()
+            self._pystream = C.PyStream(self.grid_size, self.num_plants, self.num_obstacles, int(seed),
+                                        self.thirsty_plant_prob)
         return [int(seed) + i for i in range(self.num_envs)]
 
     def _indices(self, indices):

@@ -58,3 +58,27 @@ def test_vec_env_tensor_mode_and_gym_face():
         obs, rew, term, trunc, infos = g.step(np.full(8, t % 5))
     assert trunc.all() and infos["_final_info"].all()
     g.close()
+
+
+@pytest.mark.parametrize("name", ["traj_g20_random", "traj_g20_explore", "traj_g7_explore", "traj_g21_explore"])
+def test_cpython_mode_reproduces_reference_dummyvecenv(name):
+    """reset_mode='cpython': the drop-in reproduces the REFERENCE's DummyVecEnv run
+    end to end -- the layouts come from the product's own CPython-stream generator
+    (random.seed(seed)), every obs / reward / done / terminal obs of every step
+    equals the reference's (tests/golden/traj_*.npz)."""
+    from golden_util import cfg_tuple, load
+    f = load(name)
+    G, P, O, R, C = cfg_tuple(f)
+    T, N = f["actions"].shape
+    v = PlantOSVecEnv(N, grid_size=G, num_plants=P, num_obstacles=O, lidar_range=R, lidar_channels=C,
+                      device="cuda:0", reset_mode="cpython", python_seed=int(f["seed"]))
+    obs = v.reset()
+    assert (obs == f["obs0"]).all()
+    for t in range(T):
+        obs, rew, done, infos = v.step(f["actions"][t])
+        assert (rew == f["reward"][t].astype(np.float32)).all(), t
+        assert (done == (f["terminated"][t] | f["truncated"][t]).astype(bool)).all(), t
+        for e in np.nonzero(done)[0]:
+            assert (infos[e]["terminal_observation"] == f["terminal_obs"][t, e]).all(), (t, e)
+        assert (obs == f["obs"][t]).all(), t
+    v.close()

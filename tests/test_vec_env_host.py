@@ -138,3 +138,18 @@ def test_gymnasium_vector_face():
     assert infos["_final_observation"].all()
     assert infos["final_observation"][0].shape == (87,)
     assert "TimeLimit.truncated" not in infos["final_info"][0]
+
+
+def test_stale_lazy_infos_fail_loudly():
+    v = make(3)
+    v.reset()
+    _, _, _, infos1 = v.step(np.zeros(3, np.int64))
+    d0 = infos1[0]  # read in time: served later from the host copy
+    _, _, _, infos2 = v.step(np.zeros(3, np.int64))
+    assert infos1[0] is d0 and infos1[1]["step_count"] == 1  # table fetched before expiry
+    infos2[0]
+    v.step(np.zeros(3, np.int64))
+    with pytest.raises(RuntimeError):
+        _ = [d for d in make(1).reset_infos]  # fresh env: fine
+        infos2._build._info = None
+        infos2[2]
