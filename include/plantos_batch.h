@@ -152,6 +152,22 @@ int pe_synth_actions(pe_handle* h, uint64_t seed, uint32_t t, int32_t* actions, 
  * layout); synchronizes the stream. */
 int pe_poll_errors(pe_handle* h, int32_t* bits, void* stream);
 
+/* Batched CurriculumWrapper (A2C_training.py:37-109), applied inside pe_step and
+ * every reset path: terminated is also reported when exploration_percentage >=
+ * the env's threshold (maze completed); at reset the threshold rises by the
+ * increment after a completed maze (capped), a new map starts after a completed
+ * maze or max_episodes_per_maze episodes, and otherwise the new episode keeps the
+ * previous episode's visit counts (explored map restarted; the reset obs shows the
+ * fresh visits, as the wrapper installs them after env.reset()).  The reference's
+ * "same maze" intent is not realized there either (reset seeds are ignored).
+ * Enabling (re)initializes every env's record: threshold = initial, counters 0. */
+int pe_curriculum_enable(pe_handle* h, double initial_threshold, double max_threshold,
+                         double threshold_increment, int32_t max_episodes_per_maze);
+int pe_curriculum_disable(pe_handle* h);
+/* threshold f64[n]; counters i32[n,4] = episode_count, successful_explorations,
+ * episodes_on_current_maze, flags (bit0 maze_completed, bit1 visits carried). Device. */
+int pe_curriculum_get(pe_handle* h, double* threshold, int32_t* counters, void* stream);
+
 /* Seed-exact reset layouts (host side): the reference's _generate_map
  * (plantos_env.py:338-372) on CPython's global `random` stream after
  * random.seed(seed), including CPython 3.10 set iteration order, so the maps are

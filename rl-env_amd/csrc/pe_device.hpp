@@ -65,6 +65,20 @@ struct Tables {
   uint32_t vis_pad[kMaxNW];    // empty visit row: nibble 10 in the 4 pad columns
 };
 
+// Batched CurriculumWrapper state per env (A2C_training.py:41-54), when enabled.
+struct CurRec {
+  double thr;          // exploration_threshold
+  uint32_t episodes;   // episode_count
+  uint32_t successes;  // successful_explorations
+  uint32_t on_maze;    // episodes_on_current_maze
+  uint32_t flags;      // CUR_* below
+  uint32_t pad[2];
+};
+enum : uint32_t {
+  CUR_COMPLETED = 1u,  // maze_completed
+  CUR_CARRY = 2u,      // persistent_visit_counts is not None
+};
+
 struct State {
   uint4* scal;
   double* ep_ret;
@@ -76,6 +90,7 @@ struct State {
   const signed char* ldx;  // [C][R] LIDAR offsets (generic kernel)
   const signed char* ldy;
   uint32_t* err_bits;      // OR of error flags raised since the last poll
+  CurRec* cur;             // batched CurriculumWrapper records, NULL when disabled
 };
 
 struct Rules {
@@ -84,7 +99,45 @@ struct Rules {
   uint64_t seed;
   uint32_t env_off;
   int P, O, max_steps;
+  double cur_max, cur_inc;  // CurriculumWrapper max_threshold, threshold_increment
+  int cur_max_eps;          // max_episodes_per_maze (A2C_training.py:54)
 };
+
+// CurriculumWrapper.step (A2C_training.py:97-109): exploration_percentage >= the
+// env's threshold marks the maze completed and reports terminated (the env's own
+// termination and completion bonus are untouched).  pct as the reference computes it.
+__device__ __forceinline__ bool curriculum_hit(CurRec* cur, int64_t e, double thr, int expl, int total) {
+  const double pct = ((double)expl / (double)total) * 100.0;  // plantos_env.py:331
+  if (pct >= thr) {
+    cur[e].flags |= CUR_COMPLETED;
+    return true;
+  }
+  return false;
+}
+
+// CurriculumWrapper.reset (A2C_training.py:56-95) of env e, run before its
+// env.reset(); returns true when the new episode keeps the previous episode's
+// visit counts (self.env.visit_counts = persistent_visit_counts).
+__device__ inline bool curriculum_on_reset(CurRec* cur, int64_t e, const Rules& rl) {
+  CurRec c = cur[e];
+  c.episodes += 1;
+  c.on_maze += 1;
+  const bool timeout = (int)c.on_maze >= rl.cur_max_eps;
+  bool keep = false;
+  if ((c.flags & CUR_COMPLETED) || timeout) {
+    if (c.flags & CUR_COMPLETED) {
+      c.thr = fmin(c.thr + rl.cur_inc, rl.cur_max);
+      c.successes += 1;
+    }
+    c.flags = 0;  // maze_completed = False, persistent_visit_counts = None
+    c.on_maze = 0;
+  } else {
+    keep = (c.flags & CUR_CARRY) != 0;
+    c.flags |= CUR_CARRY;  // persistent = visit_counts.copy() (tracks the live counts)
+  }
+  cur[e] = c;
+  return keep;
+}
 
 // ------------------------------------------------------------------ scalars
 struct Scal {
@@ -372,14 +425,34 @@ __device__ inline void reset_visits(const State& st, const Geo& g, const Tables*
   if (!(s.flags & F_NOROOM)) vis_set(st, g, e, s.x, s.y, 1u);
 }
 
+// Visits of a new episode: fresh (reset_visits), or -- CurriculumWrapper carrying
+// the previous episode's counts -- left in place with only the explored map
+// restarted at the rover ({rover}, bitmap mode: explored no longer follows visits).
+__device__ inline void new_episode_visits(const State& st, const Geo& g, const Tables* tab, int64_t e, Scal& s,
+                                          bool keep) {
+  if (!keep) {
+    reset_visits(st, g, tab, e, s);
+    return;
+  }
+  uint32_t* eb = st.expl + e * g.estride;
+  for (int w = 0; w < g.estride; ++w) eb[w] = 0u;
+  if (!(s.flags & F_NOROOM)) {
+    const int rc = s.x * g.G + s.y;
+    eb[rc >> 5] = 1u << (rc & 31);  // explored_map[rover] = 2 (plantos_env.py:236)
+  }
+  s.flags |= F_EXPL_BITMAP;
+}
+
 // reset() for one env (plantos_env.py:125-158), generated in place in HBM.
 // tab: the handle's tables, ideally a copy in LDS (read in every scan step).
 __device__ inline Scal reset_env(const State& st, const Geo& g, const Rules& rl, const Tables* tab, int64_t e,
                                  uint32_t episode) {
+  const bool keep = st.cur ? curriculum_on_reset(st.cur, e, rl) : false;
   uint16_t* picks = reinterpret_cast<uint16_t*>(st.vx + e * g.hstride);  // scratch (all nibbles 0 after)
-  const Scal s = gen_map(g, rl, tab, st.grid + e * g.gstride, picks, rl.env_off + (uint32_t)e, episode);
+  if (keep) picks = reinterpret_cast<uint16_t*>(st.expl + e * g.estride);  // vx holds carried counts
+  Scal s = gen_map(g, rl, tab, st.grid + e * g.gstride, picks, rl.env_off + (uint32_t)e, episode);
   if (s.flags & F_NOROOM) atomicOr(st.err_bits, F_NOROOM);
-  reset_visits(st, g, tab, e, s);
+  new_episode_visits(st, g, tab, e, s, keep);
   return s;
 }
 
@@ -390,12 +463,13 @@ __host__ __device__ constexpr int reset_scratch_bytes(int G, int WPR, int P) { r
 // the rejection-sampling scans run at LDS latency instead of HBM latency.
 __device__ inline Scal reset_env_scratch(const State& st, const Geo& g, const Rules& rl, const Tables* tab, int64_t e,
                                          uint32_t episode, uint64_t* sg) {
+  const bool keep = st.cur ? curriculum_on_reset(st.cur, e, rl) : false;
   uint16_t* picks = reinterpret_cast<uint16_t*>(sg + g.G * g.WPR);
-  const Scal s = gen_map(g, rl, tab, sg, picks, rl.env_off + (uint32_t)e, episode);
+  Scal s = gen_map(g, rl, tab, sg, picks, rl.env_off + (uint32_t)e, episode);
   if (s.flags & F_NOROOM) atomicOr(st.err_bits, F_NOROOM);
   uint64_t* gb = st.grid + e * g.gstride;
   for (int k = 0; k < g.G * g.WPR; ++k) gb[k] = sg[k];
-  reset_visits(st, g, tab, e, s);
+  new_episode_visits(st, g, tab, e, s, keep);
   return s;
 }
 

@@ -8,12 +8,14 @@
 // stores.  C-ABI: include/plantos_batch.h.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "../../include/plantos_batch.h"
 #include "lidar_tables.inc"
@@ -247,6 +249,7 @@ __global__ __launch_bounds__(kBlock) void pe_step_kernel(StepArgs a) {
     Scal s = unpack(a.st.scal[e]);
     bool term = false, trunc = false;
     double rew = transition(a, e, s, action, term, trunc);
+    if (a.st.cur) term = curriculum_hit(a.st.cur, e, a.st.cur[e].thr, s.expl, s.total) || term;
     double ret = a.st.ep_ret[e] + rew;
     a.reward[e] = (float)rew;
     a.term[e] = term;
@@ -269,7 +272,10 @@ __global__ __launch_bounds__(kBlock) void pe_step_kernel(StepArgs a) {
     }
     a.st.ep_ret[e] = ret;
     a.st.scal[e] = pack(s);
-    build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis, a.st.ldx, a.st.ldy);
+    if ((term || trunc) && a.autoreset)  // the reset() obs (fresh visits even if a curriculum carries them)
+      build_obs_fresh(a, a.st.grid + e * a.g.gstride, s, row, tdist, tpos, tvis, a.st.ldx, a.st.ldy);
+    else
+      build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis, a.st.ldx, a.st.ldy);
   }
   __syncthreads();
   const int64_t valid = a.n - e0 < kBlock ? a.n - e0 : kBlock;
@@ -409,13 +415,14 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
     }
     double rew = rl.r_step;                                        // :164
     rew += h;
-    const bool term = s.expl >= s.total;                           // :176, 244-246, 331
+    bool term = s.expl >= s.total;                                 // :176, 244-246, 331
     const bool trunc = s.step >= rl.max_steps;                     // :177
     if (term && !(s.flags & F_BONUS)) {                            // :179-181
       rew += rl.r_complete;
       s.flags |= F_BONUS;
     }
     ret += rew;
+    if (st.cur) term = curriculum_hit(st.cur, e, st.cur[e].thr, s.expl, s.total) || term;
     a.reward[e] = (float)rew;
     a.term[e] = term;
     a.trunc[e] = trunc;
@@ -433,7 +440,7 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
       s = reset_env(st, g, rl, ltab, e, s.episode);
       st.ep_ret[e] = 0.0;
       st.scal[e] = pack(s);
-      build_obs_generic(a, e, s.x, s.y, row, smem, tpos, tvis, a.st.ldx, a.st.ldy);  // fresh map: rare path
+      build_obs_fresh(a, st.grid + e * g.gstride, s, row, smem, tpos, tvis, a.st.ldx, a.st.ldy);  // rare path
     } else {
       st.ep_ret[e] = ret;
       st.scal[e] = pack(s);
@@ -531,6 +538,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
                               : (int64_t)reinterpret_cast<const int32_t*>(a.actions)[e];
     if (wv == CW) ret = st.ep_ret[e];
   }
+  double cthr = 0.0;
+  if (st.cur && live && wv == CW) cthr = st.cur[e].thr;  // CurriculumWrapper threshold
   if (llive) lw = st.scal[el];
   if constexpr ((kAblate & 64) != 0) {  // diagnostic only: whole-block streaming probe
     const uint4* gsrc = reinterpret_cast<const uint4*>(st.grid + e0 * g.gstride);
@@ -751,12 +760,13 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
       s.y = yp;
       double rew = rl.r_step;                                     // :164
       rew += h;
-      const bool term = s.expl >= s.total;                        // :176, 244-246, 331
+      bool term = s.expl >= s.total;                              // :176, 244-246, 331
       const bool trunc = s.step >= rl.max_steps;                  // :177
       if (term && !(s.flags & F_BONUS)) {                         // :179-181
         rew += rl.r_complete;
         s.flags |= F_BONUS;
       }
+      if (st.cur) term = curriculum_hit(st.cur, e, cthr, s.expl, s.total) || term;  // A2C_training.py:101-103
       ret += rew;
       a.reward[e] = (float)rew;
       a.term[e] = term;
@@ -806,7 +816,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
         PE_RSTAMP(3);
       } else {
         s = reset_env(st, g, rl, ltab, e, s.episode);
-        build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis, lldx, lldy);
+        build_obs_fresh(a, st.grid + e * g.gstride, s, row, tdist, tpos, tvis, lldx, lldy);
       }
       if (a.autoreset) {
         st.ep_ret[e] = 0.0;
@@ -868,7 +878,10 @@ __global__ __launch_bounds__(kBlock) void pe_reset_kernel(StepArgs a) {
       a.st.ep_ret[e] = 0.0;
       a.st.scal[e] = pack(s);
     }
-    if (a.obs && !(resetting && scratch_ok)) build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis, lldx, lldy);
+    if (a.obs && resetting && !scratch_ok)
+      build_obs_fresh(a, a.st.grid + e * g.gstride, s, row, tdist, tpos, tvis, lldx, lldy);
+    else if (a.obs && !resetting)
+      build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis, lldx, lldy);
   }
   if (!a.obs) return;
   __syncthreads();
@@ -897,10 +910,10 @@ __global__ __launch_bounds__(kBlock) void pe_load_maps_kernel(StepArgs a, int k,
   const Geo& g = a.g;
   const int64_t e = idx[j];
   const uint8_t* c = cells + (int64_t)j * g.GG;
+  const bool keep = a.st.cur ? curriculum_on_reset(a.st.cur, e, a.rl) : false;  // A2C_training.py:56-95
   int n_obst = 0;
   for (int row = 0; row < g.G; ++row) {
-    for (int w = 0; w < g.WPR; ++w) a.st.grid[e * g.gstride + (int64_t)row * g.WPR + w] = a.st.tab->grid_pad[w];
-    for (int w = 0; w < g.NW; ++w) a.st.vis[e * g.vstride + (int64_t)row * g.NW + w] = a.st.tab->vis_pad[w];
+    for (int w = 0; w < g.WPR; ++w) a.st.grid[e * g.gstride + (int64_t)row * g.WPR + w] = ltab->grid_pad[w];
     for (int col = 0; col < g.G; ++col) {
       int code = c[row * g.G + col] & 3;
       n_obst += code == OBST;
@@ -916,11 +929,13 @@ __global__ __launch_bounds__(kBlock) void pe_load_maps_kernel(StepArgs a, int k,
   s.episode += 1u;
   s.total = g.GG - n_obst;
   s.expl = 1;
-  vis_set(a.st, g, e, s.x, s.y, 1u);  // plantos_env.py:146-147 (explored derived, :236)
+  new_episode_visits(a.st, g, ltab, e, s, keep);  // plantos_env.py:146-147, 236
   a.st.scal[e] = pack(s);
   a.st.ep_ret[e] = 0.0;
   float* row = rows + threadIdx.x * g.DS;
-  build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis, a.st.ldx, a.st.ldy);
+  // reset() obs of the fresh episode (a carried CurriculumWrapper visit map is
+  // installed after env.reset() returned, A2C_training.py:90-91: not in this obs)
+  build_obs_fresh(a, a.st.grid + e * g.gstride, s, row, tdist, tpos, tvis, a.st.ldx, a.st.ldy);
   if (a.obs)
     for (int q = 0; q < g.D; ++q) a.obs[(int64_t)j * g.D + q] = row[q];
 }
@@ -1074,6 +1089,7 @@ struct pe_handle {
   size_t bytes;
   int variant;
   const char* kname;
+  void* cur_mem;     // CurriculumWrapper records (pe_curriculum_enable), or NULL
   size_t lds_floor;  // PE_LDS_FLOOR (diagnostics): minimum dynamic LDS per step workgroup
   int quad_waves;    // waves per workgroup of the sector kernel (4 or 8; PE_QUAD_WAVES)
 };
@@ -1296,7 +1312,8 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   g.gstride = (int64_t)align_up((size_t)G * g.WPR, 2);  // 16-B aligned env blocks (row-pair loads)
   g.vstride = (int64_t)G * g.NW;
   g.hstride = (int64_t)align_up((size_t)g.GG, 8);
-  g.estride = (int64_t)align_up((size_t)g.EW, 4);
+  // explored words; also the picks scratch of a curriculum reset that keeps visits
+  g.estride = (int64_t)align_up((size_t)std::max(g.EW, (P + 1) / 2), 4);
   if (lds_bytes(g) > 160 * 1024) {
     delete h;
     return fail(PE_ERR_ARG, "observation tile does not fit LDS");
@@ -1432,8 +1449,55 @@ int pe_destroy(pe_handle* h) {
     hipError_t e = hipFree(h->mem);
     if (e != hipSuccess) rc = hip_fail(e, "hipFree");
   }
+  if (h->cur_mem) (void)hipFree(h->cur_mem);
   delete h;
   return rc;
+}
+
+int pe_curriculum_enable(pe_handle* h, double initial_threshold, double max_threshold, double threshold_increment,
+                         int32_t max_episodes_per_maze) {
+  if (!h) return fail(PE_ERR_ARG, "null handle");
+  if (max_episodes_per_maze < 1) return fail(PE_ERR_ARG, "max_episodes_per_maze must be >= 1");
+  DeviceGuard dg(h);
+  if (dg.rc) return dg.rc;
+  if (!h->cur_mem) {
+    hipError_t me = hipMalloc(&h->cur_mem, sizeof(CurRec) * (size_t)h->n);
+    if (me != hipSuccess) {
+      h->cur_mem = nullptr;
+      return fail(PE_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(me));
+    }
+  }
+  CurRec init;
+  std::memset(&init, 0, sizeof(init));
+  init.thr = initial_threshold;  // A2C_training.py:41-54: counters 0, maze_completed False, persistent None
+  std::vector<CurRec> host((size_t)h->n, init);
+  PE_HIP(hipMemcpy(h->cur_mem, host.data(), sizeof(CurRec) * host.size(), hipMemcpyHostToDevice));
+  h->st.cur = static_cast<CurRec*>(h->cur_mem);
+  h->rl.cur_max = max_threshold;
+  h->rl.cur_inc = threshold_increment;
+  h->rl.cur_max_eps = max_episodes_per_maze;
+  return PE_OK;
+}
+
+int pe_curriculum_disable(pe_handle* h) {
+  if (!h) return fail(PE_ERR_ARG, "null handle");
+  h->st.cur = nullptr;
+  return PE_OK;
+}
+
+int pe_curriculum_get(pe_handle* h, double* threshold, int32_t* counters, void* stream) {
+  if (!h || !h->st.cur) return fail(PE_ERR_ARG, "curriculum not enabled");
+  DeviceGuard dg(h);
+  if (dg.rc) return dg.rc;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const size_t pitch = sizeof(CurRec);
+  if (threshold)
+    PE_HIP(hipMemcpy2DAsync(threshold, sizeof(double), h->st.cur, pitch, sizeof(double), (size_t)h->n,
+                            hipMemcpyDeviceToDevice, s));
+  if (counters)
+    PE_HIP(hipMemcpy2DAsync(counters, 4 * sizeof(int32_t), reinterpret_cast<char*>(h->st.cur) + 8, pitch,
+                            4 * sizeof(int32_t), (size_t)h->n, hipMemcpyDeviceToDevice, s));
+  return PE_OK;
 }
 
 int pe_seed(pe_handle* h, uint64_t seed, int32_t reset_episode_counters) {

@@ -30,6 +30,7 @@ EXPORTS = [
     "pe_get_info", "pe_get_state", "pe_set_state", "pe_load_maps", "pe_synth_actions", "pe_poll_errors",
     "pe_num_envs", "pe_kernel_variant", "pe_kernel_name", "pe_state_bytes", "pe_last_error",
     "pe_pystream_create", "pe_pystream_next", "pe_pystream_getrandbits32", "pe_pystream_destroy",
+    "pe_curriculum_enable", "pe_curriculum_disable", "pe_curriculum_get",
 ]
 
 
@@ -89,6 +90,10 @@ def lib():
     L.pe_state_bytes.restype = U64
     L.pe_last_error.argtypes = []
     L.pe_last_error.restype = ctypes.c_char_p
+    D = ctypes.c_double
+    L.pe_curriculum_enable.argtypes = [P, D, D, D, I32]
+    L.pe_curriculum_disable.argtypes = [P]
+    L.pe_curriculum_get.argtypes = [P, P, P, P]
     L.pe_pystream_create.argtypes = [CP, ctypes.c_int64, ctypes.POINTER(P)]
     L.pe_pystream_next.argtypes = [P, I32, P, P]
     L.pe_pystream_getrandbits32.argtypes = [P]
@@ -96,7 +101,8 @@ def lib():
     L.pe_pystream_destroy.argtypes = [P]
     for name in ("pe_create", "pe_destroy", "pe_seed", "pe_reset", "pe_step", "pe_get_info", "pe_get_state",
                  "pe_set_state", "pe_load_maps", "pe_synth_actions", "pe_poll_errors", "pe_pystream_create",
-                 "pe_pystream_next", "pe_pystream_destroy"):
+                 "pe_pystream_next", "pe_pystream_destroy", "pe_curriculum_enable", "pe_curriculum_disable",
+                 "pe_curriculum_get"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L

@@ -192,6 +192,27 @@ class PlantOSBatch:
             C.check(C.lib().pe_poll_errors(self.handle, ctypes.byref(bits), self._stream()), "pe_poll_errors")
         return int(bits.value)
 
+    # ----------------------------------------------------------------- curriculum
+    def enable_curriculum(self, initial_threshold=40.0, max_threshold=100.0, threshold_increment=10.0,
+                          max_episodes_per_maze=3):
+        """Batched CurriculumWrapper (A2C_training.py:37-109) on every env; the
+        defaults are the wrapper's as A2C_training.py:121 constructs it."""
+        C.check(C.lib().pe_curriculum_enable(self.handle, float(initial_threshold), float(max_threshold),
+                                             float(threshold_increment), int(max_episodes_per_maze)),
+                "pe_curriculum_enable")
+
+    def disable_curriculum(self):
+        C.check(C.lib().pe_curriculum_disable(self.handle), "pe_curriculum_disable")
+
+    def get_curriculum(self):
+        """(threshold f64[n], counters i32[n,4]: episodes, successes, episodes on maze, flags)."""
+        thr = torch.empty(self.num_envs, dtype=torch.float64, device=self.device)
+        cnt = torch.empty((self.num_envs, 4), dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            C.check(C.lib().pe_curriculum_get(self.handle, _ptr(thr), _ptr(cnt), self._stream()),
+                    "pe_curriculum_get")
+        return thr, cnt
+
     def seed(self, seed, reset_episode_counters=True):
         C.check(C.lib().pe_seed(self.handle, int(seed) & 0xFFFFFFFFFFFFFFFF, int(bool(reset_episode_counters))),
                 "pe_seed")

@@ -200,11 +200,15 @@ class PlantOSVecEnv(_VecEnvBase):
 
     def __init__(self, num_envs, grid_size=21, num_plants=8, num_obstacles=50, lidar_range=2, lidar_channels=10,
                  thirsty_plant_prob=0.7, max_steps=1000, seed=0, device=None, tensors=False, env_id_offset=0,
-                 observation_mode="lidar", render_mode=None, batch=None, reset_mode="device", python_seed=None):
+                 observation_mode="lidar", render_mode=None, batch=None, reset_mode="device", python_seed=None,
+                 curriculum=False):
         """reset_mode="device": maps from the device generator keyed by (seed, env id,
         episode) -- the throughput mode.  reset_mode="cpython": the reference's own
         layouts, seed-exact: CPython's global `random` after random.seed(python_seed)
-        (default: seed), consumed in DummyVecEnv order (pe_pystream, host side)."""
+        (default: seed), consumed in DummyVecEnv order (pe_pystream, host side).
+        curriculum=True (or a dict of CurriculumWrapper arguments) applies the batched
+        CurriculumWrapper of A2C_training.py:37-109 to every env, as
+        make_env_wrapper(use_curriculum=True) does (A2C_training.py:114-126)."""
         if observation_mode != "lidar":
             raise ValueError("only observation_mode='lidar' exists in the reference (plantos_env.py:27)")
         if reset_mode not in ("device", "cpython"):
@@ -215,6 +219,12 @@ class PlantOSVecEnv(_VecEnvBase):
             lidar_range=lidar_range, lidar_channels=lidar_channels, thirsty_plant_prob=thirsty_plant_prob,
             max_steps=max_steps, autoreset=reset_mode == "device", seed=seed, env_id_offset=env_id_offset,
             device=device)
+        if curriculum:
+            kw = dict(initial_threshold=40.0, max_threshold=100.0)  # A2C_training.py:121
+            if isinstance(curriculum, dict):
+                kw.update(curriculum)
+            self.batch.enable_curriculum(**kw)
+        self.curriculum = bool(curriculum)
         self._pystream = None
         if reset_mode == "cpython":
             self._pystream = C.PyStream(grid_size, num_plants, num_obstacles,
@@ -335,6 +345,16 @@ class PlantOSVecEnv(_VecEnvBase):
         st = self.batch.get_state()
         cells = st["cells"].cpu().numpy()
         sc = st["scalars"].cpu().numpy()
+        if attr_name in ("exploration_threshold", "episode_count", "successful_explorations",
+                         "episodes_on_current_maze", "maze_completed") and self.curriculum:
+            thr, cnt = self.batch.get_curriculum()
+            thr, cnt = thr.cpu().numpy(), cnt.cpu().numpy()
+            col = {"episode_count": 0, "successful_explorations": 1, "episodes_on_current_maze": 2}
+            if attr_name == "exploration_threshold":
+                return [float(thr[i]) for i in idx]
+            if attr_name == "maze_completed":
+                return [bool(cnt[i, 3] & 1) for i in idx]
+            return [int(cnt[i, col[attr_name]]) for i in idx]
         if attr_name == "visit_counts":
             v = st["visits"].cpu().numpy()
             return [v[i].copy() for i in idx]

@@ -11,7 +11,9 @@ TRAJ_FILES = ["traj_g20_random", "traj_g20_explore", "traj_g7_explore", "traj_g2
 
 
 def load(name):
-    return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    """All arrays of one fixture, decompressed once (NpzFile re-reads per access)."""
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as f:
+        return {k: f[k] for k in f.files}
 
 
 def cfg_tuple(f):

@@ -82,3 +82,32 @@ def test_cpython_mode_reproduces_reference_dummyvecenv(name):
             assert (infos[e]["terminal_observation"] == f["terminal_obs"][t, e]).all(), (t, e)
         assert (obs == f["obs"][t]).all(), t
     v.close()
+
+
+@pytest.mark.parametrize("name", ["curriculum_g20_explore", "curriculum_g7_explore", "curriculum_g20_random"])
+def test_curriculum_reproduces_reference_wrapper(name):
+    """PlantOSVecEnv(curriculum=True, reset_mode='cpython') against the reference's
+    CurriculumWrapper + env in a DummyVecEnv loop (tests/golden/curriculum_*.npz):
+    obs (incl. carried visit slices), rewards, curriculum terminations, terminal
+    obs, per-step thresholds and the final wrapper counters."""
+    from golden_util import cfg_tuple, load
+    f = load(name)
+    G, P, O, R, C = cfg_tuple(f)
+    T, N = f["actions"].shape
+    v = PlantOSVecEnv(N, grid_size=G, num_plants=P, num_obstacles=O, lidar_range=R, lidar_channels=C,
+                      device="cuda:0", reset_mode="cpython", python_seed=int(f["seed"]), curriculum=True)
+    assert (v.reset() == f["obs0"]).all()
+    for t in range(T):
+        obs, rew, done, infos = v.step(f["actions"][t])
+        assert (rew == f["reward"][t].astype(np.float32)).all(), t
+        assert (done == (f["terminated"][t] | f["truncated"][t]).astype(bool)).all(), t
+        for e in np.nonzero(done)[0]:
+            assert (infos[e]["terminal_observation"] == f["terminal_obs"][t, e]).all(), (t, e)
+        assert (obs == f["obs"][t]).all(), t
+        if t % 25 == 0 or done.any():
+            assert v.get_attr("exploration_threshold") == list(f["threshold"][t]), t
+    thr, cnt = v.batch.get_curriculum()
+    assert (cnt.cpu().numpy() == f["final_counters"]).all()
+    vs = v.get_attr("visit_counts")
+    assert [int(x.sum()) for x in vs] == list(f["visits_sum"][T - 1])
+    v.close()

@@ -399,6 +399,68 @@ def gen_traj(cfg, n_envs, steps, seed, policy):
     print(f"traj_{cfg}_{policy}: {n_envs}x{steps}, resets={len(reset_maps)}, term={int(te.sum())}")
 
 
+def load_curriculum_wrapper():
+    """The reference's own CurriculumWrapper class (A2C_training.py:37-109), compiled
+    from the reference file: only that class definition is executed (the module's
+    stable_baselines3 / matplotlib imports and directory creation are skipped --
+    those packages are absent here and not part of the wrapper)."""
+    import ast
+    import gymnasium as gym_shim
+    path = os.path.join(REF, "A2C_training.py")
+    tree = ast.parse(open(path).read())
+    node = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "CurriculumWrapper")
+    ns = {"gym": gym_shim, "np": np}
+    exec(compile(ast.Module(body=[node], type_ignores=[]), path, "exec"), ns)  # noqa: S102
+    return ns["CurriculumWrapper"]
+
+
+def gen_curriculum(cfg, n_envs, steps, seed, policy):
+    """DummyVecEnv over CurriculumWrapper(fork env, 40, 100) (A2C_training.py:114-126
+    with use_curriculum=True; Monitor omitted: it does not change the step data)."""
+    CW = load_curriculum_wrapper()
+    envs = [CW(make(ForkEnv, cfg), initial_threshold=40.0, max_threshold=100.0) for _ in range(n_envs)]
+    G = envs[0].env.grid_size
+    random.seed(seed)
+    np.random.seed(seed + 7)  # the wrapper's np.random.randint "maze seeds" (ignored by the env)
+    rng = np.random.default_rng(seed + 1000)
+    obs0 = np.array([w.reset()[0] for w in envs], np.float32)
+    D = obs0.shape[1]
+    acts = np.zeros((steps, n_envs), np.int32)
+    obs = np.zeros((steps, n_envs, D), np.float32)
+    term_obs = np.zeros((steps, n_envs, D), np.float32)
+    rew = np.zeros((steps, n_envs), np.float64)
+    te = np.zeros((steps, n_envs), np.uint8)
+    tr = np.zeros((steps, n_envs), np.uint8)
+    thr = np.zeros((steps, n_envs), np.float64)
+    visits_sum = np.zeros((steps, n_envs), np.int64)
+    for t in range(steps):
+        for i, w in enumerate(envs):
+            if policy == "random":
+                a = int(rng.integers(0, 5))
+            else:
+                a = bfs_action(w.env) if rng.random() < 0.9 else int(rng.integers(0, 5))
+            acts[t, i] = a
+            o, r, a_te, a_tr, _ = w.step(a)
+            rew[t, i] = r
+            te[t, i] = a_te
+            tr[t, i] = a_tr
+            if a_te or a_tr:
+                term_obs[t, i] = o
+                o, _ = w.reset()
+            obs[t, i] = o
+            thr[t, i] = w.exploration_threshold
+            visits_sum[t, i] = int(w.env.visit_counts.sum())
+    fin = np.array([[w.episode_count, w.successful_explorations, w.episodes_on_current_maze,
+                     int(w.maze_completed) | (2 * int(w.persistent_visit_counts is not None))] for w in envs],
+                   np.int32)
+    np.savez_compressed(
+        os.path.join(OUT, f"curriculum_{cfg}_{policy}.npz"), config=np.array(CONFIGS[cfg], np.int32),
+        seed=np.int64(seed), obs0=obs0, actions=acts, obs=obs, terminal_obs=term_obs, reward=rew,
+        terminated=te, truncated=tr, threshold=thr, visits_sum=visits_sum, final_counters=fin,
+        next_u32=np.int64(random.getrandbits(32)))
+    print(f"curriculum_{cfg}_{policy}: {n_envs}x{steps}, term={int(te.sum())}, thr_max={thr.max()}, G={G}")
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     gen_kat()
@@ -420,6 +482,9 @@ def main():
     gen_traj("g20", 3, 900, 5, "explore")
     gen_traj("g7", 4, 300, 3, "explore")
     gen_traj("g21", 2, 400, 8, "explore")
+    gen_curriculum("g20", 4, 1500, 11, "explore")
+    gen_curriculum("g7", 6, 400, 12, "explore")
+    gen_curriculum("g20", 3, 2100, 13, "random")
 
 
 if __name__ == "__main__":
