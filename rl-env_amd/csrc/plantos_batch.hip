@@ -47,6 +47,7 @@ struct StepArgs {
   double* ep_ret_out;
   int32_t* ep_len_out;
   int32_t* tinfo;       // terminal _get_info rows of done envs (may be NULL)
+  int stagger;          // sector kernel: start delay per block quarter, units of 512 cycles
   const uint8_t* mask;  // reset kernel
 };
 
@@ -217,7 +218,16 @@ __device__ __forceinline__ void store_tile(const float* rows, float* dst, int va
       const int n4 = total >> 2;
       const float4* s4 = reinterpret_cast<const float4*>(rows);
       float4* d4 = reinterpret_cast<float4*>(dst);
+#ifndef PE_TEMPORAL_OBS
+      // non-temporal: the obs stream (28 MB per step at the headline batch) must not
+      // evict the envs' state from L2 / the Infinity Cache (measured +12%, profiles/)
+      typedef float v4f __attribute__((ext_vector_type(4)));
+      const v4f* sv = reinterpret_cast<const v4f*>(rows);
+      v4f* dv = reinterpret_cast<v4f*>(dst);
+      for (int k = threadIdx.x; k < n4; k += blockDim.x) __builtin_nontemporal_store(sv[k], &dv[k]);
+#else
       for (int k = threadIdx.x; k < n4; k += blockDim.x) d4[k] = s4[k];
+#endif
       for (int k = (n4 << 2) + threadIdx.x; k < total; k += blockDim.x) dst[k] = rows[k];
     } else {
       for (int k = threadIdx.x; k < total; k += blockDim.x) dst[k] = rows[k];
@@ -525,6 +535,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
   // role for round 2: LT = NW threads per env (env le, part sub), so each load
   // instruction reads LT consecutive rows of 64/LT envs instead of one row of 64.
   PE_STAMP(0);
+  if (a.stagger) {  // de-phase the resident workgroups of a CU (speed only)
+    const int q = (int)(blockIdx.x * 4 / gridDim.x);
+    for (int i = 0; i < q * a.stagger; ++i) __builtin_amdgcn_s_sleep(8);
+  }
   constexpr int LT = NW;
   const int le = threadIdx.x / LT, sub = threadIdx.x % LT;
   const int64_t el = e0 + le;
@@ -1092,6 +1106,7 @@ struct pe_handle {
   void* cur_mem;     // CurriculumWrapper records (pe_curriculum_enable), or NULL
   size_t lds_floor;  // PE_LDS_FLOOR (diagnostics): minimum dynamic LDS per step workgroup
   int quad_waves;    // waves per workgroup of the sector kernel (4 or 8; PE_QUAD_WAVES)
+  int stagger;       // PE_STAGGER (experimental): sector-kernel start delay per block quarter
 };
 
 namespace {
@@ -1147,6 +1162,7 @@ StepArgs base_args(const pe_handle* h) {
   a.rl = h->rl;
   a.n = h->n;
   a.autoreset = h->cfg.autoreset;
+  a.stagger = h->stagger;
   return a;
 }
 
@@ -1373,6 +1389,8 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   const char* qw = std::getenv("PE_QUAD_WAVES");
   // measured (profiles/r1c-r1e): 4 waves win at C=16, 8 waves at C=64
   h->quad_waves = qw ? (std::atoi(qw) == 4 ? 4 : 8) : (C >= 64 ? 8 : 4);
+  const char* sg = std::getenv("PE_STAGGER");
+  h->stagger = sg ? std::atoi(sg) : 0;
   const char* lf = std::getenv("PE_LDS_FLOOR");
   h->lds_floor = lf ? (size_t)std::strtoul(lf, nullptr, 10) : 0;
   if (h->lds_floor > 160 * 1024) h->lds_floor = 160 * 1024;
