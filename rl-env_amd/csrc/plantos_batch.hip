@@ -218,9 +218,22 @@ __device__ __forceinline__ void store_tile(const float* rows, float* dst, int va
       const int n4 = total >> 2;
       const float4* s4 = reinterpret_cast<const float4*>(rows);
       float4* d4 = reinterpret_cast<float4*>(dst);
-#ifndef PE_TEMPORAL_OBS
-      // non-temporal: the obs stream (28 MB per step at the headline batch) must not
-      // evict the envs' state from L2 / the Infinity Cache (measured +12%, profiles/)
+#if !defined(PE_OBS_STORE_ASM) && !defined(PE_OBS_STORE_NT) && !defined(PE_TEMPORAL_OBS)
+#define PE_OBS_STORE_ASM "sc1"
+#endif
+#if defined(PE_OBS_STORE_ASM)
+      // the obs stream (28 MB per step at the headline batch) is written with sc1
+      // (write-through; the line is dropped from the XCD's L2) so it does not evict
+      // the envs' state from L2 / the Infinity Cache: plain stores 12.8 us, nt 11.4,
+      // sc1 11.1 us per step (profiles/r1i_store_policy.json).  Inline asm: the
+      // compiler does not count these in vmcnt; the reset path waits explicitly.
+      typedef float v4f __attribute__((ext_vector_type(4)));
+      const v4f* sv = reinterpret_cast<const v4f*>(rows);
+      for (int k = threadIdx.x; k < n4; k += blockDim.x) {
+        const v4f v = sv[k];
+        asm volatile("global_store_dwordx4 %0, %1, off " PE_OBS_STORE_ASM ::"v"(d4 + k), "v"(v) : "memory");
+      }
+#elif defined(PE_OBS_STORE_NT)
       typedef float v4f __attribute__((ext_vector_type(4)));
       const v4f* sv = reinterpret_cast<const v4f*>(rows);
       v4f* dv = reinterpret_cast<v4f*>(dst);
