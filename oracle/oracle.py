@@ -67,6 +67,14 @@ def lib():
         L.po_bench.restype = ctypes.c_double
         L.po_synth_action.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]
         L.po_synth_action.restype = ctypes.c_int32
+        L.po_mt_seed_genrand.argtypes = [ctypes.POINTER(POMt), ctypes.c_uint32]
+        L.po_np_random.argtypes = [ctypes.POINTER(POMt)]
+        L.po_np_random.restype = ctypes.c_double
+        L.po_np_randint.argtypes = [ctypes.POINTER(POMt), ctypes.c_int32]
+        L.po_np_randint.restype = ctypes.c_int32
+        L.po_mcts_search.argtypes = [ctypes.POINTER(POConfig), P, P, P, P, ctypes.POINTER(POMt), ctypes.c_int32,
+                                     ctypes.c_double, ctypes.c_int32, P, P, P]
+        L.po_mcts_search.restype = ctypes.c_int32
         _lib = L
     return _lib
 
@@ -103,6 +111,40 @@ class MT:
 
     def u32(self):
         return lib().po_mt_u32(ctypes.byref(self.s))
+
+
+class NpMT:
+    """numpy legacy RandomState stream (np.random.seed(int) semantics) on the oracle's MT."""
+
+    def __init__(self, seed):
+        self.s = POMt()
+        lib().po_mt_seed_genrand(ctypes.byref(self.s), seed)
+
+    def state(self):
+        """(key uint32[624], pos) exactly as numpy's get_state() reports them."""
+        return np.array(self.s.mt[:], np.uint32), int(self.s.index)
+
+    def random(self):
+        return lib().po_np_random(ctypes.byref(self.s))
+
+    def randint(self, n):
+        return lib().po_np_randint(ctypes.byref(self.s), n)
+
+
+def mcts_search(cfg, cells, visits, explored, scal, rng, n_sims, c_param, max_depth):
+    """MCTS.search (mcts_custom_trainer.py:91-139) of one env; rng (NpMT) advances.
+    Returns (action, order[5], visits[5], value[5]) -- root children in insertion order."""
+    cells = np.ascontiguousarray(cells, np.uint8)
+    visits = np.ascontiguousarray(visits, np.int32)
+    explored = np.ascontiguousarray(explored, np.int8)
+    sc = np.zeros(NSCAL, np.int32)
+    sc[:len(scal)] = scal
+    order = np.zeros(5, np.int32)
+    cv = np.zeros(5, np.int32)
+    cval = np.zeros(5, np.float64)
+    a = lib().po_mcts_search(ctypes.byref(cfg), _p(cells), _p(visits), _p(explored), _p(sc), ctypes.byref(rng.s),
+                             n_sims, c_param, max_depth, _p(order), _p(cv), _p(cval))
+    return a, order, cv, cval
 
 
 class Batch:

@@ -186,7 +186,7 @@ static void step_with(const po_config* c, const lidar_tab* t, uint8_t* cells, in
             rew += c->r_water_empty;                               /* :221-222 */
         }
     }
-    obs_with(c, t, cells, visits, scal, obs);                      /* :173 */
+    if (obs) obs_with(c, t, cells, visits, scal, obs);             /* :173 */
     int32_t info[5];
     po_info(c, cells, explored, info);                             /* :174 */
     double pct = ((double)info[3] / (double)info[4]) * 100.0;      /* :331 */
@@ -201,6 +201,10 @@ static void step_with(const po_config* c, const lidar_tab* t, uint8_t* cells, in
 
 void po_step(const po_config* c, uint8_t* cells, int32_t* visits, int8_t* explored, int32_t* scal,
              int64_t action, float* obs, double* reward, uint8_t* terminated, uint8_t* truncated) {
+    if (!obs) {                                                    /* no observation wanted */
+        step_with(c, NULL, cells, visits, explored, scal, action, NULL, reward, terminated, truncated);
+        return;
+    }
     lidar_tab t = tab_new(c);
     step_with(c, &t, cells, visits, explored, scal, action, obs, reward, terminated, truncated);
     tab_free(&t);
@@ -250,6 +254,12 @@ static void mt_init_by_array(po_mt* m, const uint32_t* key, int len) {
         }
     }
     m->mt[0] = 0x80000000u;
+    m->index = 624;
+}
+
+/* numpy RandomState.seed(int): init_genrand, pos = 624 (numpy legacy seeding). */
+void po_mt_seed_genrand(po_mt* m, uint32_t seed) {
+    mt_init_genrand(m, seed);
     m->index = 624;
 }
 

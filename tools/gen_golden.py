@@ -461,6 +461,110 @@ def gen_curriculum(cfg, n_envs, steps, seed, policy):
     print(f"curriculum_{cfg}_{policy}: {n_envs}x{steps}, term={int(te.sum())}, thr_max={thr.max()}, G={G}")
 
 
+def load_mcts():
+    """The reference's MCTS module (mcts_custom_trainer.py), imported through the shim.
+    Its sim envs are built from the module-level name `PlantOSEnv` (:227-233); that name
+    is pointed at the fork env, whose watering of a hydrated plant returns R_MISTAKE
+    (gradio-app/plantos_env_new.py:236-245) -- with the root env a random rollout that
+    waters a hydrated plant raises TypeError (plantos_env.py:217-220) and aborts the
+    search.  best_action (:62-69) is wrapped to RECORD the root's children (action,
+    visits, value in insertion order); the returned action is the reference's own."""
+    import mcts_custom_trainer as M
+    M.PlantOSEnv = ForkEnv
+    rec = []
+    orig = M.MCTSNode.best_action
+
+    def best_action(self):
+        if self.parent is None:
+            rec.append([(a, c.visits, c.value) for a, c in self.children.items()])
+        return orig(self)
+
+    M.MCTSNode.best_action = best_action
+    return M, rec
+
+
+def np_state_crc(st):
+    import zlib
+    return zlib.crc32(np.ascontiguousarray(st[1], np.uint32).tobytes())
+
+
+def gen_mcts(name, cfg, n_sims, max_depth, chains, decisions, seed, inject_cases=0, c_param=1.414):
+    """MCTS.search (mcts_custom_trainer.py:91-139) decisions of the reference.
+
+    chains: episodes from reset (random.seed(seed+k) map, np.random.seed(seed+100+k)
+    stream), `decisions` searches each, the real env stepped with the chosen action
+    between them (train_mcts, :298-302).  inject_cases: single searches from
+    injected states (step counts near max_steps, nearly explored maps), each with
+    its own np.random.seed."""
+    M, rec = load_mcts()
+    G = CONFIGS[cfg][0]
+    A = {k: [] for k in ["chain", "cseed", "cells", "visits", "explored", "scal", "action", "order",
+                         "cvisits", "cvalue", "pos_out", "crc_out"]}
+
+    def one(env, mcts, chain, cseed):
+        A["chain"].append(chain)
+        A["cseed"].append(cseed)
+        A["cells"].append(cells_of(env))
+        A["visits"].append(env.visit_counts.astype(np.int32).copy())
+        A["explored"].append(env.explored_map.astype(np.int8).copy())
+        A["scal"].append([env.rover_pos[0], env.rover_pos[1], env.step_count, env.total_collisions,
+                          int(env.collided_with_wall), int(env.completion_bonus_given)])
+        rec.clear()
+        a = mcts.search(None)
+        kids = rec[0]
+        order = np.full(5, -1, np.int32)
+        cv = np.zeros(5, np.int32)
+        cval = np.zeros(5, np.float64)
+        for j, (ca, vis, val) in enumerate(kids):
+            order[j], cv[j], cval[j] = ca, vis, val
+        A["action"].append(a)
+        A["order"].append(order)
+        A["cvisits"].append(cv)
+        A["cvalue"].append(cval)
+        st = np.random.get_state()
+        A["pos_out"].append(st[2])
+        A["crc_out"].append(np_state_crc(st))
+        return a
+
+    nterm = 0
+    for k in range(chains):
+        env = make(ForkEnv, cfg)
+        random.seed(seed + k)
+        env.reset()
+        np.random.seed(seed + 100 + k)
+        mcts = M.MCTS(env, n_simulations=n_sims, c_param=c_param, max_depth=max_depth)
+        for d in range(decisions):
+            a = one(env, mcts, k, seed + 100 + k if d == 0 else -1)
+            _, _, te, tr, _ = env.step(int(a))
+            if te or tr:
+                nterm += 1
+                break
+    rng = np.random.default_rng(seed + 7)
+    for i in range(inject_cases):
+        env = make(ForkEnv, cfg)
+        random.seed(seed + 1000 + i)
+        env.reset()
+        st = random_state(rng, cfg, "complete" if i % 3 == 2 else "random")
+        if i % 4 == 1:
+            st["step"] = int(rng.choice([995, 998, 999, 1000, 1004]))
+        inject(env, st)
+        np.random.seed(seed + 2000 + i)
+        mcts = M.MCTS(env, n_simulations=n_sims, c_param=c_param, max_depth=max_depth)
+        one(env, mcts, chains + i, seed + 2000 + i)
+    np.savez_compressed(
+        os.path.join(OUT, f"mcts_{name}.npz"), config=np.array(CONFIGS[cfg], np.int32),
+        n_sims=np.int32(n_sims), max_depth=np.int32(max_depth), c_param=np.float64(c_param),
+        chain=np.array(A["chain"], np.int32), cseed=np.array(A["cseed"], np.int64),
+        cells=np.array(A["cells"], np.uint8).reshape(-1, G, G),
+        visits=np.array(A["visits"], np.int32).reshape(-1, G, G),
+        explored=np.array(A["explored"], np.int8).reshape(-1, G, G),
+        scal=np.array(A["scal"], np.int32).reshape(-1, 6), action=np.array(A["action"], np.int32),
+        order=np.array(A["order"], np.int32).reshape(-1, 5), cvisits=np.array(A["cvisits"], np.int32).reshape(-1, 5),
+        cvalue=np.array(A["cvalue"], np.float64).reshape(-1, 5), pos_out=np.array(A["pos_out"], np.int32),
+        crc_out=np.array(A["crc_out"], np.uint32))
+    print(f"mcts_{name}: {len(A['action'])} searches, episodes ended={nterm}")
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     gen_kat()
@@ -487,5 +591,16 @@ def main():
     gen_curriculum("g20", 3, 2100, 13, "random")
 
 
+def main_mcts():
+    os.makedirs(OUT, exist_ok=True)
+    gen_mcts("g7", "g7", 30, 40, 4, 40, 500, inject_cases=30)
+    gen_mcts("g20", "g20", 50, 100, 3, 12, 600, inject_cases=24)
+    gen_mcts("g25", "g25", 50, 100, 1, 8, 700)
+    gen_mcts("g20d", "g20", 100, 50, 1, 4, 800)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["mcts"]:
+        main_mcts()
+    else:
+        main()
