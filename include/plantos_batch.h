@@ -17,6 +17,7 @@
  *   pe_load_maps    reset() with a host-supplied layout (seed-exact CPython stream mode)
  *   pe_seed         VecEnv.seed / reset(seed=...)    (the reference ignores it for maps)
  *   pe_destroy      PlantOSEnv.close                 plantos_env.py:522-528
+ *   pe_mcts_*       MCTS.search for every env at once mcts_custom_trainer.py:72-243
  *
  * Conventions
  *  - Every array argument is a DEVICE pointer (caller-owned, e.g. a torch tensor on
@@ -182,6 +183,33 @@ int pe_pystream_next(pe_pystream* s, int32_t k, uint8_t* cells, int32_t* rover);
 /* random.getrandbits(32) on the stream (tests pin the number of draws consumed) */
 uint32_t pe_pystream_getrandbits32(pe_pystream* s);
 int pe_pystream_destroy(pe_pystream* s);
+
+/* Batched MCTS (mcts_custom_trainer.py:72-243): one MCTS.search per env of `h`,
+ * every env with its own tree, its own clone of the env state (_copy_env_state
+ * :221-243: position, plants, obstacles, explored map, visit counts and step count
+ * copied; collision/bonus flags start cleared) and its own np.random stream
+ * (numpy legacy RandomState: np.random.seed(int) = MT19937 init_genrand; random()
+ * and randint(n) as numpy draws them).  UCB1 selection (:37-60), expansion of a
+ * random untried action (:117-125), the 70/30 least-visited-neighbour rollout
+ * policy (:141-219, +500 when a rollout ends fully explored), backpropagation and
+ * best_action (:62-69) are the reference's, bit for bit.  Sim envs water with the
+ * fork's semantics (hydrated plant: R_MISTAKE).  Searches read the live state of
+ * `h` and never modify it; they step nothing: apply the actions with pe_step.
+ * Scratch: (G*G + 2*max_depth + 2) * 4 + (n_simulations + 1) * 32 + 2504 bytes/env. */
+typedef struct pe_mcts pe_mcts;
+int pe_mcts_create(pe_handle* h, int32_t n_simulations, double c_param, int32_t max_depth, pe_mcts** out);
+int pe_mcts_destroy(pe_mcts* m);
+/* np.random.seed(seeds[e]) for env e (HOST array of n, or NULL: base_seed + e). */
+int pe_mcts_seed(pe_mcts* m, const uint32_t* seeds, uint32_t base_seed, void* stream);
+/* Stream state in numpy's own terms (get_state()[1:3]): key u32[n,624], pos i32[n].
+ * HOST arrays; synchronous. */
+int pe_mcts_set_rng(pe_mcts* m, const uint32_t* key, const int32_t* pos);
+int pe_mcts_get_rng(pe_mcts* m, uint32_t* key, int32_t* pos);
+/* One search per env (mask u8[n] or NULL = all): actions i32[n] (masked-out envs
+ * untouched); optional root children in insertion order: order i32[n,5] (action,
+ * -1 pad), visits i32[n,5], value f64[n,5].  Device pointers. */
+int pe_mcts_search(pe_mcts* m, const uint8_t* mask, int32_t* actions, int32_t* root_order, int32_t* root_visits,
+                   double* root_value, void* stream);
 
 /* Introspection for tests / benchmarks. */
 int32_t pe_num_envs(const pe_handle* h);

@@ -12,8 +12,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "plantos_batch.hip")
 SRC_HOST = os.path.join(HERE, "csrc", "pe_pystream.cpp")
-DEPS = [SRC, SRC_HOST, os.path.join(HERE, "csrc", "pe_device.hpp"), os.path.join(HERE, "csrc", "pe_fast.hpp"), os.path.join(REPO, "include", "plantos_batch.h"),
-        os.path.join(HERE, "tools_gen_lidar.py")]
+SRC_MCTS = os.path.join(HERE, "csrc", "pe_mcts.hip")
+DEPS = [SRC, SRC_HOST, SRC_MCTS] + [os.path.join(HERE, "csrc", f) for f in
+                                    ("pe_device.hpp", "pe_fast.hpp", "pe_quad.hpp", "pe_handle.hpp")] + [
+    os.path.join(REPO, "include", "plantos_batch.h"), os.path.join(HERE, "tools_gen_lidar.py")]
 OUT = os.path.join(HERE, "plantos_amd", "libplantos_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
@@ -25,7 +27,7 @@ def build(force=False, verbose=False):
     deps = DEPS + [os.path.join(HERE, "csrc", "lidar_tables.inc")]
     if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= max(os.path.getmtime(d) for d in deps):
         return OUT
-    cmd = [HIPCC] + FLAGS + ["-o", OUT, SRC, SRC_HOST]
+    cmd = [HIPCC] + FLAGS + ["-o", OUT, SRC, SRC_MCTS, SRC_HOST]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

@@ -1,0 +1,25 @@
+// pe_handle.hpp -- the handle behind the opaque pe_handle* of include/plantos_batch.h
+// (shared by the translation units of libplantos_hip.so; not part of the ABI).
+#pragma once
+#include "../../include/plantos_batch.h"
+#include "pe_device.hpp"
+
+struct pe_handle {
+  int device;
+  int n;
+  pe_config cfg;
+  pe::Geo g;
+  pe::Rules rl;
+  pe::State st;
+  void* mem;
+  size_t bytes;
+  int variant;
+  const char* kname;
+  void* cur_mem;     // CurriculumWrapper records (pe_curriculum_enable), or NULL
+  size_t lds_floor;  // PE_LDS_FLOOR (diagnostics): minimum dynamic LDS per step workgroup
+  int quad_waves;    // waves per workgroup of the sector kernel (4 or 8; PE_QUAD_WAVES)
+  int stagger;       // PE_STAGGER (experimental): sector-kernel start delay per block quarter
+};
+
+// pe_internal_set_error (plantos_batch.hip): records pe_last_error() for this thread.
+extern "C" int pe_internal_set_error(int code, const char* msg);

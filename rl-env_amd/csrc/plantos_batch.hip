@@ -1105,22 +1105,7 @@ __global__ void pe_synth_kernel(int n, uint64_t seed, uint32_t env_off, uint32_t
 }  // namespace
 
 // ====================================================================== host side
-struct pe_handle {
-  int device;
-  int n;
-  pe_config cfg;
-  Geo g;
-  Rules rl;
-  State st;
-  void* mem;
-  size_t bytes;
-  int variant;
-  const char* kname;
-  void* cur_mem;     // CurriculumWrapper records (pe_curriculum_enable), or NULL
-  size_t lds_floor;  // PE_LDS_FLOOR (diagnostics): minimum dynamic LDS per step workgroup
-  int quad_waves;    // waves per workgroup of the sector kernel (4 or 8; PE_QUAD_WAVES)
-  int stagger;       // PE_STAGGER (experimental): sector-kernel start delay per block quarter
-};
+#include "pe_handle.hpp"
 
 namespace {
 

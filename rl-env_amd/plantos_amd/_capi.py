@@ -31,6 +31,7 @@ EXPORTS = [
     "pe_num_envs", "pe_kernel_variant", "pe_kernel_name", "pe_state_bytes", "pe_last_error",
     "pe_pystream_create", "pe_pystream_next", "pe_pystream_getrandbits32", "pe_pystream_destroy",
     "pe_curriculum_enable", "pe_curriculum_disable", "pe_curriculum_get",
+    "pe_mcts_create", "pe_mcts_destroy", "pe_mcts_seed", "pe_mcts_set_rng", "pe_mcts_get_rng", "pe_mcts_search",
 ]
 
 
@@ -99,10 +100,17 @@ def lib():
     L.pe_pystream_getrandbits32.argtypes = [P]
     L.pe_pystream_getrandbits32.restype = U32
     L.pe_pystream_destroy.argtypes = [P]
+    L.pe_mcts_create.argtypes = [P, I32, D, I32, ctypes.POINTER(P)]
+    L.pe_mcts_destroy.argtypes = [P]
+    L.pe_mcts_seed.argtypes = [P, P, U32, P]
+    L.pe_mcts_set_rng.argtypes = [P, P, P]
+    L.pe_mcts_get_rng.argtypes = [P, P, P]
+    L.pe_mcts_search.argtypes = [P, P, P, P, P, P, P]
     for name in ("pe_create", "pe_destroy", "pe_seed", "pe_reset", "pe_step", "pe_get_info", "pe_get_state",
                  "pe_set_state", "pe_load_maps", "pe_synth_actions", "pe_poll_errors", "pe_pystream_create",
                  "pe_pystream_next", "pe_pystream_destroy", "pe_curriculum_enable", "pe_curriculum_disable",
-                 "pe_curriculum_get"):
+                 "pe_curriculum_get", "pe_mcts_create", "pe_mcts_destroy", "pe_mcts_seed", "pe_mcts_set_rng",
+                 "pe_mcts_get_rng", "pe_mcts_search"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
