@@ -18,14 +18,15 @@
 // position p: words [0,p) already hold the NEXT round's words, [p,624) this round's;
 // the next output is temper(mt[p]).  A draw regenerates its own word (the twist done
 // one word at a time, which is order-equivalent to numpy's block twist), so no lane
-// ever stops for a 624-word twist.  Draws are produced 8 at a time with all 16 loads
-// in flight together; a drawn word is written back only when it is consumed, so an
-// unfinished batch leaves the stream exactly at its first unconsumed position.
+// ever stops for a 624-word twist.  Draws are generated ahead into a per-lane LDS ring
+// (wave-uniform top-ups, all loads of a top-up in flight together); the unconsumed
+// tail is rewound at the end, so the stream stops exactly at its first unconsumed draw.
 // mt[625] keeps this round's mt[0] (overwritten at position 0) so the host can give
 // the state back in numpy's own terms (pe_mcts_get_rng).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -66,6 +67,10 @@ struct MctsArgs {
   Rules rl;
   int n;
   uint32_t* cellw;
+  uint8_t* cellb;   // [N][ggp] clone bytes (LDS path)
+  uint32_t* csim;   // [N][G*G] (LDS path)
+  uint32_t* csg;    // [N][G*G] (LDS path)
+  int ggp;
   uint2* ulog;
   MNode* nodes;
   uint32_t* rng;
@@ -93,62 +98,105 @@ __device__ __forceinline__ uint32_t twist(uint32_t cur, uint32_t nxt, uint32_t f
 }
 
 // One env's np.random stream, device form (see the file comment).
+__device__ __forceinline__ uint32_t untemper(uint32_t y) {
+  y ^= y >> 18;
+  y ^= (y << 15) & 0xefc60000u;
+  uint32_t t = y;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) t = y ^ ((t << 7) & 0x9d2c5680u);
+  y = t;
+  return y ^ (y >> 11) ^ (y >> 22);
+}
+
+constexpr int kRing = 32;  // buffered draws per lane (LDS ring)
+constexpr int kTop = 16;   // draws per top-up (all 32 loads in flight together)
+constexpr int kLow = 8;    // the wave tops up when any lane has fewer left (> draws of one step, typically)
+
+// One env's np.random stream, device form (see the file comment).  Draws are
+// generated ahead into a lane-private LDS ring; generation writes the next-round
+// words at once, and close() rewinds the generated-but-unconsumed tail (the raw
+// word is untemper(output)), so the stored stream stops exactly at the first
+// unconsumed draw.  Top-ups are wave-uniform (top_up_if_low) so a wave pays one
+// memory round trip for all its lanes instead of one per lane.
 struct NpStream {
   uint32_t* mt;
-  int p, base, ib;  // p: position after the buffered batch; base: position of out[0]
-  uint32_t cur;     // mt[p] (this round's word at p)
-  uint32_t raw0;    // this round's word at position 0, if the batch holds position 0
-  uint32_t out[8], nw[8];
+  uint32_t* ring;
+  int p;               // position of the next draw to generate
+  uint32_t cur;        // mt[p] (the current-round word at p)
+  int head, cnt;       // ring read slot, draws buffered
+  uint32_t saved_prev; // mt[625] before the last generation of position 0
 
-  __device__ void open(uint32_t* m) {
+  __device__ void open(uint32_t* m, uint32_t* r) {
     mt = m;
+    ring = r;
     p = (int)m[kMtN];
     cur = m[p];
-    base = p;
-    ib = 8;  // empty
+    head = 0;
+    cnt = 0;
+    saved_prev = m[kMtN + 1];
   }
-  __device__ void refill() {
-    uint32_t nx[8], far[8];
+  __device__ void top_up() {  // kTop draws (requires cnt <= kRing - kTop)
+    uint32_t nx[kTop], far[kTop];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < kTop; ++k) {
       int i1 = p + 1 + k, i2 = p + kMtM + k;
       i1 -= i1 >= kMtN ? kMtN : 0;
       i2 -= i2 >= kMtN ? kMtN : 0;
       nx[k] = mt[i1];
       far[k] = mt[i2];
     }
-    base = p;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      if (p + k == 0 || p + k == kMtN) raw0 = cur;
-      nw[k] = twist(cur, nx[k], far[k]);
-      out[k] = temper(cur);
+    for (int k = 0; k < kTop; ++k) {
+      int pos = p + k;
+      pos -= pos >= kMtN ? kMtN : 0;
+      if (pos == 0) {  // this round's mt[0], kept for pe_mcts_get_rng
+        saved_prev = mt[kMtN + 1];
+        mt[kMtN + 1] = cur;
+      }
+      mt[pos] = twist(cur, nx[k], far[k]);
+      ring[(head + cnt + k) & (kRing - 1)] = temper(cur);
       cur = nx[k];
     }
-    p += 8;
+    p += kTop;
     p -= p >= kMtN ? kMtN : 0;
-    ib = 0;
+    cnt += kTop;
+  }
+  __device__ void top_up_if_low() {
+    if (__any(cnt < kLow) && cnt <= kRing - kTop) top_up();
+  }
+  // one draw straight from the stream (ring empty: a long rejection streak, rare)
+  __device__ uint32_t gen_direct() {
+    int i1 = p + 1, i2 = p + kMtM;
+    i1 -= i1 >= kMtN ? kMtN : 0;
+    i2 -= i2 >= kMtN ? kMtN : 0;
+    const uint32_t nxt = mt[i1], far = mt[i2];
+    if (p == 0) {
+      saved_prev = mt[kMtN + 1];
+      mt[kMtN + 1] = cur;
+    }
+    mt[p] = twist(cur, nxt, far);
+    const uint32_t v = temper(cur);
+    cur = nxt;
+    p = i1;
+    return v;
   }
   __device__ uint32_t next() {
-    if (ib == 8) refill();
-    uint32_t o = 0, w = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint32_t m = 0u - (uint32_t)(k == ib);
-      o |= out[k] & m;
-      w |= nw[k] & m;
-    }
-    int pos = base + ib;
-    pos -= pos >= kMtN ? kMtN : 0;
-    mt[pos] = w;
-    if (pos == 0) mt[kMtN + 1] = raw0;  // this round's mt[0], kept for pe_mcts_get_rng
-    ++ib;
-    return o;
+    if (cnt == 0) return gen_direct();
+    const uint32_t v = ring[head];
+    head = (head + 1) & (kRing - 1);
+    --cnt;
+    return v;
   }
   __device__ void close() {
-    int pos = ib == 8 ? p : base + ib;  // first unconsumed position
-    pos -= pos >= kMtN ? kMtN : 0;
-    mt[kMtN] = (uint32_t)pos;
+    int q = p - cnt;
+    q += q < 0 ? kMtN : 0;
+    for (int j = 0; j < cnt; ++j) {  // rewind the unconsumed tail
+      int pos = q + j;
+      pos -= pos >= kMtN ? kMtN : 0;
+      mt[pos] = untemper(ring[(head + j) & (kRing - 1)]);
+      if (pos == 0) mt[kMtN + 1] = saved_prev;
+    }
+    mt[kMtN] = (uint32_t)q;
   }
   // np.random.random(): 53 bits from two draws
   __device__ double random() {
@@ -177,15 +225,12 @@ struct Sim {
   bool cur_expl, bonus;
 };
 
-// N, E, S, W neighbours (plantos_env.py:186) and the rover's own cell.
-__device__ __forceinline__ void load_cells(const uint32_t* cw, int G, const Sim& s, uint32_t w[5]) {
-  const int c = s.x * G + s.y;
-  w[0] = s.x > 0 ? cw[c - G] : kOffMap;
-  w[1] = s.y + 1 < G ? cw[c + 1] : kOffMap;
-  w[2] = s.x + 1 < G ? cw[c + G] : kOffMap;
-  w[3] = s.y > 0 ? cw[c - 1] : kOffMap;
-  w[4] = cw[c];
-}
+// What one sim step reads: the rover's N, E, S, W neighbours (plantos_env.py:186)
+// and its own cell (index 4).  Off-map neighbours read as obstacles (:193-195).
+struct Nbr {
+  uint32_t code[5], vis[5];  // cell code, exact visit count
+  uint32_t expl;             // bit q: explored_map > 0
+};
 
 __device__ __forceinline__ uint32_t sel5(const uint32_t w[5], int k) {
   uint32_t v = 0;
@@ -194,42 +239,142 @@ __device__ __forceinline__ uint32_t sel5(const uint32_t w[5], int k) {
   return v;
 }
 
+__device__ __forceinline__ int nbr_cell(int c, int G, int q) {
+  return q == 0 ? c - G : (q == 1 ? c + 1 : (q == 2 ? c + G : (q == 3 ? c - 1 : c)));
+}
+
+__device__ __forceinline__ bool nbr_on_map(const Sim& s, int G, int q) {
+  return q == 0 ? s.x > 0 : (q == 1 ? s.y + 1 < G : (q == 2 ? s.x + 1 < G : (q == 3 ? s.y > 0 : true)));
+}
+
+// Sim cells in global memory (any G): u32 words, exact visits; undo log of
+// (cell, old word).
+struct GCells {
+  uint32_t* cw;
+  uint2* lg;
+  int nlog, G, c;
+  uint32_t w[5];
+  __device__ void load(const Sim& s, Nbr& nb) {
+    c = s.x * G + s.y;
+    nb.expl = 0;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      w[q] = nbr_on_map(s, G, q) ? cw[nbr_cell(c, G, q)] : kOffMap;
+      nb.code[q] = (w[q] & kCodeMask) >> kCodeShift;
+      nb.vis[q] = w[q] & kVisMask;
+      nb.expl |= (w[q] & kExpl) ? 1u << q : 0u;
+    }
+  }
+  // visit_counts[new] += 1, explored_map[new] = 2, explored_map[old] = 1 (:198-203)
+  __device__ void move(int q, bool set_old) {
+    if (set_old) {
+      lg[nlog++] = make_uint2((uint32_t)c, w[4]);
+      cw[c] = w[4] | kExpl;
+    }
+    const int nc = nbr_cell(c, G, q);
+    const uint32_t nw = sel5(w, q);
+    lg[nlog++] = make_uint2((uint32_t)nc, nw);
+    cw[nc] = (nw | kExpl) + 1u;
+  }
+  __device__ void water() {  // thirsty -> hydrated (fork :237-240)
+    lg[nlog++] = make_uint2((uint32_t)c, w[4]);
+    cw[c] = (w[4] & ~kCodeMask) | ((uint32_t)HYD << kCodeShift);
+  }
+  __device__ void undo() {
+    for (int k = nlog - 1; k >= 0; --k) {
+      const uint2 u = lg[k];
+      cw[u.x] = u.y;
+    }
+    nlog = 0;
+  }
+};
+
+// Sim cells in LDS (G <= 64): one byte per cell = visits min(v,31) (bits 0-4) |
+// explored << 5 | code << 6.  A field of 31 means "31 or more": the exact count is
+// the clone's word (cellw) or, once this simulation has bumped the cell, csim
+// (valid where csg holds the simulation's stamp).  Undo = copy the clone's pristine
+// bytes (cellb, global, 16-B loads) back over the lane's LDS cells.
+constexpr uint32_t kLSat = 31u, kLExpl = 32u;
+constexpr int kLCodeShift = 6;
+
+__device__ __forceinline__ uint32_t sat_byte(uint32_t w) {
+  const uint32_t v = w & kVisMask;
+  return (v < kLSat ? v : kLSat) | ((w & kExpl) ? kLExpl : 0u) | (((w & kCodeMask) >> kCodeShift) << kLCodeShift);
+}
+
+struct LCells {
+  uint8_t* cb;            // this lane's cells (LDS, 16-B aligned)
+  const uint4* pristine;  // this lane's clone bytes (global)
+  const uint32_t* cw;     // exact clone words (global)
+  uint32_t* csim;         // exact sim counts of bumped saturated cells (global)
+  uint32_t* csg;          // their stamps
+  int G, c, nchunk;       // nchunk = padded cells / 16
+  uint32_t stamp;
+  uint32_t b[5];
+  __device__ uint32_t exact(int i) const { return csg[i] == stamp ? csim[i] : (cw[i] & kVisMask); }
+  __device__ void load(const Sim& s, Nbr& nb) {
+    c = s.x * G + s.y;
+    nb.expl = 0;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      b[q] = nbr_on_map(s, G, q) ? (uint32_t)cb[nbr_cell(c, G, q)] : ((uint32_t)OBST << kLCodeShift);
+      nb.code[q] = b[q] >> kLCodeShift;
+      const uint32_t f = b[q] & kLSat;
+      nb.vis[q] = f < kLSat ? f : exact(nbr_cell(c, G, q));
+      nb.expl |= (b[q] & kLExpl) ? 1u << q : 0u;
+    }
+  }
+  __device__ void move(int q, bool set_old) {
+    if (set_old) cb[c] = (uint8_t)(b[4] | kLExpl);
+    const int nc = nbr_cell(c, G, q);
+    const uint32_t nb_ = sel5(b, q);
+    const uint32_t f = nb_ & kLSat;
+    uint32_t nv = nb_ | kLExpl;
+    if (f + 1u < kLSat) {
+      nv += 1u;
+    } else {
+      const uint32_t x = f < kLSat ? kLSat : exact(nc) + 1u;
+      nv |= kLSat;
+      csim[nc] = x;
+      csg[nc] = stamp;
+    }
+    cb[nc] = (uint8_t)nv;
+  }
+  __device__ void water() {
+    cb[c] = (uint8_t)((b[4] & ~(3u << kLCodeShift)) | ((uint32_t)HYD << kLCodeShift));
+  }
+  __device__ void undo() {
+    uint4* dst = reinterpret_cast<uint4*>(cb);
+#pragma unroll 8
+    for (int k = 0; k < nchunk; ++k) dst[k] = pristine[k];  // LDS stores never alias the loads
+    ++stamp;
+  }
+};
+
 // PlantOSEnv.step on the sim env (plantos_env.py:160-183; watering of the fork,
 // plantos_env_new.py:236-245).  Only what MCTS reads is produced: reward,
 // terminated, truncated (the observation and info dict are never used by the search).
-__device__ double sim_step(const MctsArgs& a, uint32_t* cw, uint2* lg, int& nlog, Sim& s, int total, int act,
-                           const uint32_t w[5], bool& te, bool& tr) {
-  const Rules& rl = a.rl;
-  const int G = a.g.G;
+template <class CS>
+__device__ double sim_step(const Rules& rl, CS& cs, Sim& s, int total, int act, const Nbr& nb, bool& te, bool& tr) {
   s.step += 1;                                                   // :162
   double r = rl.r_step;                                          // :164
   if (act < 4) {
-    const uint32_t nw = sel5(w, act);
-    if (((nw & kCodeMask) >> kCodeShift) != (uint32_t)OBST) {   // in bounds, not an obstacle (:193-195)
-      const int dx = act == 0 ? -1 : (act == 2 ? 1 : 0), dy = act == 1 ? 1 : (act == 3 ? -1 : 0);
-      const int oc = s.x * G + s.y, nc = oc + dx * G + dy;
-      const bool never = (nw & kVisMask) == 0u;                  // :197
-      if (!s.cur_expl) {                                         // explored_map[old] = 1 (:198)
-        lg[nlog++] = make_uint2((uint32_t)oc, w[4]);
-        cw[oc] = w[4] | kExpl;
-        s.expl += 1;
-      }
-      lg[nlog++] = make_uint2((uint32_t)nc, nw);
-      s.expl += (nw & kExpl) ? 0 : 1;                            // explored_map[new] = 2 (:200)
-      cw[nc] = (nw | kExpl) + 1u;                                // visit_counts[new] += 1 (:203)
-      s.x += dx;
-      s.y += dy;
+    if (sel5(nb.code, act) != (uint32_t)OBST) {                 // in bounds, not an obstacle (:193-195)
+      const bool never = sel5(nb.vis, act) == 0u;                // :197
+      const bool new_unexpl = ((nb.expl >> act) & 1u) == 0u;
+      cs.move(act, !s.cur_expl);                                 // :198-203
+      s.expl += (s.cur_expl ? 0 : 1) + (new_unexpl ? 1 : 0);
+      s.x += act == 0 ? -1 : (act == 2 ? 1 : 0);
+      s.y += act == 1 ? 1 : (act == 3 ? -1 : 0);
       s.cur_expl = true;
       r += never ? rl.r_exploration : rl.r_revisit;              // :204-207
     } else {
       r += rl.r_invalid;                                         // :208-211
     }
   } else {
-    const uint32_t code = (w[4] & kCodeMask) >> kCodeShift;
+    const uint32_t code = nb.code[4];
     if (code == (uint32_t)THIRSTY) {                             // fork :237-240
-      const int oc = s.x * G + s.y;
-      lg[nlog++] = make_uint2((uint32_t)oc, w[4]);
-      cw[oc] = (w[4] & ~kCodeMask) | ((uint32_t)HYD << kCodeShift);
+      cs.water();
       r += rl.r_goal;
     } else if (code == (uint32_t)HYD) {
       r += rl.r_mistake;                                         // fork :241-242
@@ -237,10 +382,13 @@ __device__ double sim_step(const MctsArgs& a, uint32_t* cw, uint2* lg, int& nlog
       r += rl.r_water_empty;                                     // :221-222
     }
   }
-  const double pct = ((double)s.expl / (double)total) * 100.0;  // :320-331
-  te = pct >= 100.0;                                             // :176, 244-246
+  // exploration_percentage = explored / total * 100 >= 100 (:320-331, 176, 244-246)
+  // holds exactly when explored >= total: for e < t the f64 quotient is at most
+  // 1 - 2^-53 and its product with 100 rounds below 100
+  const bool full = s.expl >= total;
+  te = full;
   tr = s.step >= rl.max_steps;                                   // :177
-  if (pct >= 100.0 && !s.bonus) {                                // :179-181
+  if (full && !s.bonus) {                                        // :179-181
     r += rl.r_complete;
     s.bonus = true;
   }
@@ -264,7 +412,12 @@ __global__ void pe_mcts_clone_kernel(MctsArgs a) {
     ex = (a.st.expl[e * g.estride + (c >> 5)] >> (c & 31)) & 1u;
   else
     ex = v > 0u;  // explored_map > 0 <=> visit > 0 (derived mode)
-  a.cellw[e * (int64_t)g.GG + c] = (v & kVisMask) | (code << kCodeShift) | (ex ? kExpl : 0u);
+  const uint32_t w = (v & kVisMask) | (code << kCodeShift) | (ex ? kExpl : 0u);
+  a.cellw[e * (int64_t)g.GG + c] = w;
+  if (a.cellb) {
+    a.cellb[e * (int64_t)a.ggp + c] = (uint8_t)sat_byte(w);
+    a.csg[e * (int64_t)g.GG + c] = 0u;
+  }
 }
 
 __device__ __forceinline__ MNode load_node(const MNode* T, int i) {
@@ -304,112 +457,128 @@ __device__ __forceinline__ int kid_at(const MNode& nd, int j) {
   return v;
 }
 
-// MCTS.search (:91-139) for the lane's env.
-__global__ __launch_bounds__(64) void pe_mcts_search_kernel(MctsArgs a) {
+// MCTS.search (:91-139) for env e with its sim cells in `cs`.  The four phases of a
+// simulation are one loop of sim steps: each iteration picks the step's action by
+// the lane's current phase (tree descent, expansion, rollout) and all lanes then
+// run the same sim step together, whatever phase each is in.
+enum : int { PH_SELECT = 0, PH_EXPAND = 1, PH_ROLLOUT = 2, PH_DONE = 3 };
+
+template <class CS>
+__device__ void search_env(const MctsArgs& a, int64_t e, CS& cs, uint32_t* ring) {
 #pragma clang fp contract(off)
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= a.n) return;
-  if (a.mask && !a.mask[e]) return;
-  const Geo& g = a.g;
-  const int G = g.G;
   const Scal s0 = unpack(a.st.scal[e]);
   const int total = s0.total;
-  uint32_t* cw = a.cellw + e * (int64_t)g.GG;
-  uint2* lg = a.ulog + e * (int64_t)(a.max_depth + 4);
   MNode* T = a.nodes + e * (int64_t)(a.n_sims + 1);
   NpStream rng;
-  rng.open(a.rng + e * (int64_t)kRngStride);
-  const bool root_expl = (cw[s0.x * G + s0.y] & kExpl) != 0u;
+  rng.open(a.rng + e * (int64_t)kRngStride, ring);
+  Nbr nb;
+  Sim s;
+  s.x = s0.x;
+  s.y = s0.y;
+  cs.load(s, nb);
+  const bool root_expl = (nb.expl >> 4) & 1u;
 
   store_node(T, 0, fresh_node(0xFFFF, 0xFF));
   int nn = 1;
   for (int sim = 0; sim < a.n_sims; ++sim) {
-    Sim s;
     s.x = s0.x;
     s.y = s0.y;
     s.step = s0.step;
     s.expl = s0.expl;
     s.cur_expl = root_expl;
     s.bonus = false;  // a fresh PlantOSEnv: completion_bonus_given False (:221-243)
-    int nlog = 0;
-    int node = 0, depth = 0;
-    bool te = false, tr = false;
-    uint32_t w[5];
-    MNode nd = load_node(T, 0);
-    // 1. selection (:106-114)
-    while ((nd.untried & 7u) == 0u && nd.nkid > 0 && depth < a.max_depth) {
-      const double lv = a.logt[nd.visits];
-      int best = -1;
-      double bw = 0.0;
-      for (int j = 0; j < nd.nkid; ++j) {
-        const int ci = kid_at(nd, j);
-        const MNode ch = load_node(T, ci);
-        double wgt;
-        if (ch.visits == 0) {
-          wgt = INFINITY;
-        } else {
-          const double exploitation = ch.value / (double)ch.visits;                 // :55
-          const double exploration = a.c * sqrt(lv / (double)ch.visits);          // :56
-          wgt = exploitation + exploration;                                         // :57
-        }
-        if (best < 0 || wgt > bw) {  // max(): the first maximal child (:60)
-          best = ci;
-          bw = wgt;
-        }
-      }
-      node = best;
-      nd = load_node(T, node);
-      load_cells(cw, G, s, w);
-      sim_step(a, cw, lg, nlog, s, total, nd.action, w, te, tr);
-      depth += 1;
-      if (te || tr) break;
-    }
-    // 2. expansion (:117-125); depth is not advanced
-    if ((nd.untried & 7u) > 0u && depth < a.max_depth) {
-      const int cnt = (int)(nd.untried & 7u);
-      const int k = rng.randint(cnt);
-      const int act = (int)((nd.untried >> (3 + 3 * k)) & 7u);
-      const uint32_t below = nd.untried & ((1u << (3 + 3 * k)) - 1u) & ~7u;
-      const uint32_t above = (nd.untried >> (3 + 3 * (k + 1))) << (3 + 3 * k);
-      nd.untried = below | above | (uint32_t)(cnt - 1);
-      const int ci = nn++;
-#pragma unroll
-      for (int j = 0; j < 5; ++j)
-        if (j == nd.nkid) nd.kid[j] = (uint16_t)ci;
-      nd.nkid += 1;
-      store_node(T, node, nd);
-      load_cells(cw, G, s, w);
-      sim_step(a, cw, lg, nlog, s, total, act, w, te, tr);
-      store_node(T, ci, fresh_node(node, act));
-      node = ci;
-    }
-    // 3. rollout (:141-168)
+    int node = 0, depth = 0, phase = PH_SELECT;
     double tot = 0.0;
-    for (int d = depth; d < a.max_depth; ++d) {
-      load_cells(cw, G, s, w);
-      int act;
-      if (rng.random() < 0.7) {                                  // :180
-        // _exploration_heuristic (:187-219): first strictly least-visited valid move
-        int best = -1;
-        uint32_t minv = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const bool ok = ((w[q] & kCodeMask) >> kCodeShift) != (uint32_t)OBST;
-          const uint32_t v = w[q] & kVisMask;
-          if (ok && (best < 0 || v < minv)) {
-            best = q;
-            minv = v;
+    MNode nd = load_node(T, 0);
+    while (phase != PH_DONE) {
+      rng.top_up_if_low();
+      int act = -1;
+      if (phase == PH_SELECT) {
+        // 1. selection (:106-114): descend while fully expanded
+        if ((nd.untried & 7u) == 0u && nd.nkid > 0 && depth < a.max_depth) {
+          const double lv = a.logt[nd.visits];
+          int best = -1;
+          double bw = 0.0;
+          for (int j = 0; j < nd.nkid; ++j) {
+            const int ci = kid_at(nd, j);
+            const MNode ch = load_node(T, ci);
+            double wgt;
+            if (ch.visits == 0) {
+              wgt = INFINITY;
+            } else {
+              const double exploitation = ch.value / (double)ch.visits;             // :55
+              const double exploration = a.c * sqrt(lv / (double)ch.visits);      // :56
+              wgt = exploitation + exploration;                                     // :57
+            }
+            if (best < 0 || wgt > bw) {  // max(): the first maximal child (:60)
+              best = ci;
+              bw = wgt;
+            }
           }
+          node = best;
+          nd = load_node(T, node);
+          act = nd.action;
+        } else {
+          phase = PH_EXPAND;
         }
-        act = best >= 0 ? best : rng.randint(5);
-      } else {
-        act = rng.randint(5);                                    // :183
       }
-      const double r = sim_step(a, cw, lg, nlog, s, total, act, w, te, tr);
-      tot += r;
-      if (te || tr) {
-        if (((double)s.expl / (double)total) * 100.0 >= 100.0) tot += 500.0;  // :160-163
-        break;
+      if (phase == PH_EXPAND) {
+        // 2. expansion (:117-125); depth is not advanced
+        if ((nd.untried & 7u) > 0u && depth < a.max_depth) {
+          const int cnt = (int)(nd.untried & 7u);
+          const int k = rng.randint(cnt);
+          act = (int)((nd.untried >> (3 + 3 * k)) & 7u);
+          const uint32_t below = nd.untried & ((1u << (3 + 3 * k)) - 1u) & ~7u;
+          const uint32_t above = (nd.untried >> (3 + 3 * (k + 1))) << (3 + 3 * k);
+          nd.untried = below | above | (uint32_t)(cnt - 1);
+          const int ci = nn++;
+#pragma unroll
+          for (int j = 0; j < 5; ++j)
+            if (j == nd.nkid) nd.kid[j] = (uint16_t)ci;
+          nd.nkid += 1;
+          store_node(T, node, nd);
+          store_node(T, ci, fresh_node(node, act));
+          node = ci;
+        } else {
+          phase = PH_ROLLOUT;
+        }
+      }
+      cs.load(s, nb);
+      if (phase == PH_ROLLOUT) {
+        // 3. rollout (:141-168), depth counts on from the descent
+        if (depth >= a.max_depth) {
+          phase = PH_DONE;
+        } else if (rng.random() < 0.7) {                          // :180
+          // _exploration_heuristic (:187-219): first strictly least-visited valid move
+          int best = -1;
+          uint32_t minv = 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (nb.code[q] != (uint32_t)OBST && (best < 0 || nb.vis[q] < minv)) {
+              best = q;
+              minv = nb.vis[q];
+            }
+          }
+          act = best >= 0 ? best : rng.randint(5);
+        } else {
+          act = rng.randint(5);                                   // :183
+        }
+      }
+      if (phase == PH_DONE) break;
+      bool te, tr;
+      const double r = sim_step(a.rl, cs, s, total, act, nb, te, tr);
+      if (phase == PH_SELECT) {
+        depth += 1;
+        if (te || tr) phase = PH_EXPAND;
+      } else if (phase == PH_EXPAND) {
+        phase = PH_ROLLOUT;
+      } else {
+        tot += r;
+        depth += 1;
+        if (te || tr) {
+          if (s.expl >= total) tot += 500.0;  // exploration_percentage >= 100 (:160-163)
+          phase = PH_DONE;
+        }
       }
     }
     // 4. backpropagation (:130-134)
@@ -420,11 +589,7 @@ __global__ __launch_bounds__(64) void pe_mcts_search_kernel(MctsArgs a) {
       store_node(T, i, b);
       i = b.parent;
     }
-    // restore the sim env for the next simulation (a new _copy_env_state)
-    for (int k = nlog - 1; k >= 0; --k) {
-      const uint2 u = lg[k];
-      cw[u.x] = u.y;
-    }
+    cs.undo();  // the next simulation starts from a fresh copy (:104)
   }
   // best_action (:62-69)
   const MNode root = load_node(T, 0);
@@ -456,6 +621,49 @@ __global__ __launch_bounds__(64) void pe_mcts_search_kernel(MctsArgs a) {
       if (a.rvalue) a.rvalue[e * 5 + j] = has ? ch.value : 0.0;
     }
   }
+}
+
+// Any G: sim cells in global memory.
+__global__ __launch_bounds__(64) void pe_mcts_search_kernel(MctsArgs a) {
+  __shared__ uint32_t ring[64 * kRing];
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.n) return;
+  if (a.mask && !a.mask[e]) return;
+  GCells cs;
+  cs.cw = a.cellw + e * (int64_t)a.g.GG;
+  cs.lg = a.ulog + e * (int64_t)(a.max_depth + 4);
+  cs.nlog = 0;
+  cs.G = a.g.G;
+  search_env(a, e, cs, ring + threadIdx.x * kRing);
+}
+
+// G <= 64: the workgroup's 64 sim envs live in LDS (lane-private regions): the
+// rollout's neighbour reads and updates never leave the CU.
+__global__ __launch_bounds__(64) void pe_mcts_search_lds_kernel(MctsArgs a) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  const int lane = threadIdx.x;
+  const int64_t e0 = (int64_t)blockIdx.x * 64;
+  const int ggp = a.ggp;
+  // cooperative copy of the 64 clones (coalesced 16-B reads)
+  const int nchunk = ggp / 16;
+  const int64_t lim = ((int64_t)a.n - e0 < 64 ? (int64_t)a.n - e0 : 64) * nchunk;
+  const uint4* src = reinterpret_cast<const uint4*>(a.cellb + e0 * ggp);
+  uint4* dst = reinterpret_cast<uint4*>(lds);
+  for (int64_t i = lane; i < lim; i += 64) dst[i] = src[i];
+  __syncthreads();
+  const int64_t e = e0 + lane;
+  if (e >= a.n) return;
+  if (a.mask && !a.mask[e]) return;
+  LCells cs;
+  cs.cb = lds + lane * ggp;
+  cs.pristine = reinterpret_cast<const uint4*>(a.cellb + e * ggp);
+  cs.cw = a.cellw + e * (int64_t)a.g.GG;
+  cs.csim = a.csim + e * (int64_t)a.g.GG;
+  cs.csg = a.csg + e * (int64_t)a.g.GG;
+  cs.G = a.g.G;
+  cs.nchunk = nchunk;
+  cs.stamp = 1;
+  search_env(a, e, cs, reinterpret_cast<uint32_t*>(lds + 64 * ggp) + lane * kRing);
 }
 
 // np.random.seed(seed) (init_genrand, pos 624) then the pending block twist, giving
@@ -548,12 +756,19 @@ void device_to_np(const uint32_t* dev, uint32_t* key, int32_t* pos) {
 
 }  // namespace
 
+constexpr size_t kMctsLdsMax = 64 * 1024;  // >= 2 workgroups per CU
+
 struct pe_mcts {
   pe_handle* h;
+  int force_global;  // PE_MCTS_GLOBAL=1: the global-memory sim cells even when LDS fits
   int n_sims, max_depth;
   double c;
   void* mem;
   uint32_t* cellw;
+  uint8_t* cellb;   // [N][ggp] clone bytes (LDS path)
+  uint32_t* csim;   // [N][G*G] (LDS path)
+  uint32_t* csg;    // [N][G*G] (LDS path)
+  int ggp;
   uint2* ulog;
   MNode* nodes;
   uint32_t* rng;
@@ -571,12 +786,14 @@ int pe_mcts_create(pe_handle* h, int32_t n_simulations, double c_param, int32_t 
   if (db.err != hipSuccess) return hip_fail(db.err, "hipSetDevice");
   const size_t n = (size_t)h->n, GG = (size_t)h->g.GG;
   auto al = [](size_t v) { return (v + 255) / 256 * 256; };
+  const size_t ggp = (GG + 15) / 16 * 16;
   const size_t b_cell = al(n * GG * 4), b_log = al(n * (size_t)(max_depth + 4) * 8),
+               b_lds = al(n * ggp) + 2 * al(n * GG * 4),
                b_node = al(n * (size_t)(n_simulations + 1) * sizeof(MNode)), b_rng = al(n * kRngStride * 4),
                b_log_t = al((size_t)(n_simulations + 1) * 8);
   pe_mcts* m = new (std::nothrow) pe_mcts();
   if (!m) return fail(PE_ERR_NOMEM, "host allocation failed");
-  hipError_t e = hipMalloc(&m->mem, b_cell + b_log + b_node + b_rng + b_log_t);
+  hipError_t e = hipMalloc(&m->mem, b_cell + b_log + b_node + b_rng + b_log_t + b_lds);
   if (e != hipSuccess) {
     delete m;
     return fail(PE_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
@@ -587,7 +804,13 @@ int pe_mcts_create(pe_handle* h, int32_t n_simulations, double c_param, int32_t 
   m->nodes = reinterpret_cast<MNode*>(p + b_cell + b_log);
   m->rng = reinterpret_cast<uint32_t*>(p + b_cell + b_log + b_node);
   m->logt = reinterpret_cast<double*>(p + b_cell + b_log + b_node + b_rng);
+  char* q = p + b_cell + b_log + b_node + b_rng + b_log_t;
+  m->cellb = reinterpret_cast<uint8_t*>(q);
+  m->csim = reinterpret_cast<uint32_t*>(q + al(n * ggp));
+  m->csg = reinterpret_cast<uint32_t*>(q + al(n * ggp) + al(n * GG * 4));
+  m->ggp = (int)ggp;
   m->h = h;
+  m->force_global = getenv("PE_MCTS_GLOBAL") && atoi(getenv("PE_MCTS_GLOBAL")) != 0;
   m->n_sims = n_simulations;
   m->max_depth = max_depth;
   m->c = c_param;
@@ -697,9 +920,20 @@ int pe_mcts_search(pe_mcts* m, const uint8_t* mask, int32_t* actions, int32_t* r
   a.rvalue = root_value;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t cells = (int64_t)h->n * h->g.GG;
+  const size_t lds = 64 * ((size_t)m->ggp + 4 * (size_t)kRing);
+  const bool use_lds = h->g.G <= 64 && lds <= kMctsLdsMax && !m->force_global;
+  if (use_lds) {
+    a.cellb = m->cellb;
+    a.csim = m->csim;
+    a.csg = m->csg;
+    a.ggp = m->ggp;
+  }
   if (cells > 0) {
     hipLaunchKernelGGL(pe_mcts_clone_kernel, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(pe_mcts_search_kernel, dim3((unsigned)((h->n + 63) / 64)), dim3(64), 0, s, a);
+    if (use_lds)
+      hipLaunchKernelGGL(pe_mcts_search_lds_kernel, dim3((unsigned)((h->n + 63) / 64)), dim3(64), lds, s, a);
+    else
+      hipLaunchKernelGGL(pe_mcts_search_kernel, dim3((unsigned)((h->n + 63) / 64)), dim3(64), 0, s, a);
   }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? PE_OK : hip_fail(e, "pe_mcts_search");
