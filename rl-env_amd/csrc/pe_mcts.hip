@@ -70,7 +70,7 @@ struct MctsArgs {
   uint8_t* cellb;   // [N][ggp] clone bytes (LDS path)
   uint32_t* csim;   // [N][G*G] (LDS path)
   uint32_t* csg;    // [N][G*G] (LDS path)
-  int ggp;
+  int ggp, ldsp;    // global / LDS per-env byte strides of the clone bytes
   uint2* ulog;
   MNode* nodes;
   uint32_t* rng;
@@ -109,18 +109,23 @@ __device__ __forceinline__ uint32_t untemper(uint32_t y) {
 }
 
 constexpr int kRing = 32;  // buffered draws per lane (LDS ring)
-constexpr int kTop = 16;   // draws per top-up (all 32 loads in flight together)
+constexpr int kTop = 16;   // draws per top-up: one 16-aligned block of stream positions
 constexpr int kLow = 8;    // the wave tops up when any lane has fewer left (> draws of one step, typically)
+static_assert(kMtN % kTop == 0 && kRngStride % 4 == 0, "16-aligned blocks never straddle the wrap");
 
 // One env's np.random stream, device form (see the file comment).  Draws are
-// generated ahead into a lane-private LDS ring; generation writes the next-round
-// words at once, and close() rewinds the generated-but-unconsumed tail (the raw
-// word is untemper(output)), so the stored stream stops exactly at the first
-// unconsumed draw.  Top-ups are wave-uniform (top_up_if_low) so a wave pays one
-// memory round trip for all its lanes instead of one per lane.
+// generated ahead into an LDS ring, one 16-aligned block of stream positions per
+// top-up: the block's words, its successors and its "far" words (+397) come in as
+// 16-B loads and the next-round words go out as 16-B stores.  Top-ups are
+// wave-uniform (top_up_if_low), so a wave pays one memory round trip for all its
+// lanes.  Until the position is 16-aligned (a stream left mid-block by a previous
+// search) draws come one at a time (gen_direct).  close() rewinds the
+// generated-but-unconsumed tail (raw word = untemper(output)), so the stored stream
+// stops exactly at the first unconsumed draw.  The ring is [slot][lane] interleaved
+// (a top-up's 64 lanes write one slot row: no bank conflicts).
 struct NpStream {
   uint32_t* mt;
-  uint32_t* ring;
+  uint32_t* ring;      // &ring_base[lane]; slot k at ring[k * 64]
   int p;               // position of the next draw to generate
   uint32_t cur;        // mt[p] (the current-round word at p)
   int head, cnt;       // ring read slot, draws buffered
@@ -135,36 +140,58 @@ struct NpStream {
     cnt = 0;
     saved_prev = m[kMtN + 1];
   }
-  __device__ void top_up() {  // kTop draws (requires cnt <= kRing - kTop)
+  __device__ void top_up() {  // positions p .. p+15 (p % 16 == 0, cnt <= kRing - kTop)
+    const uint4* m4 = reinterpret_cast<const uint4*>(mt);
     uint32_t nx[kTop], far[kTop];
+    // successors p+1 .. p+16: the block itself shifted by one, plus the next block's first word
+    const uint4 b0 = m4[p / 4], b1 = m4[p / 4 + 1], b2 = m4[p / 4 + 2], b3 = m4[p / 4 + 3];
+    int pn = p + kTop;
+    pn -= pn >= kMtN ? kMtN : 0;
+    const uint32_t w16 = mt[pn];
+    // far words p+397 .. p+412 lie in the 4-word chunks starting at p+396, +400, ..., +412
+    uint4 f[5];
 #pragma unroll
-    for (int k = 0; k < kTop; ++k) {
-      int i1 = p + 1 + k, i2 = p + kMtM + k;
-      i1 -= i1 >= kMtN ? kMtN : 0;
-      i2 -= i2 >= kMtN ? kMtN : 0;
-      nx[k] = mt[i1];
-      far[k] = mt[i2];
+    for (int k = 0; k < 5; ++k) {
+      int q = p + 396 + 4 * k;
+      q -= q >= kMtN ? kMtN : 0;
+      q -= q >= kMtN ? kMtN : 0;
+      f[k] = m4[q / 4];
     }
+    const uint32_t blk[16] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w,
+                              b2.x, b2.y, b2.z, b2.w, b3.x, b3.y, b3.z, b3.w};
+    const uint32_t fw[20] = {f[0].x, f[0].y, f[0].z, f[0].w, f[1].x, f[1].y, f[1].z, f[1].w,
+                             f[2].x, f[2].y, f[2].z, f[2].w, f[3].x, f[3].y, f[3].z, f[3].w,
+                             f[4].x, f[4].y, f[4].z, f[4].w};
 #pragma unroll
     for (int k = 0; k < kTop; ++k) {
-      int pos = p + k;
-      pos -= pos >= kMtN ? kMtN : 0;
-      if (pos == 0) {  // this round's mt[0], kept for pe_mcts_get_rng
-        saved_prev = mt[kMtN + 1];
-        mt[kMtN + 1] = cur;
-      }
-      mt[pos] = twist(cur, nx[k], far[k]);
-      ring[(head + cnt + k) & (kRing - 1)] = temper(cur);
+      nx[k] = k + 1 < kTop ? blk[k + 1] : w16;
+      far[k] = fw[k + 1];
+    }
+    if (p == 0) {  // this round's mt[0], kept for pe_mcts_get_rng
+      saved_prev = mt[kMtN + 1];
+      mt[kMtN + 1] = cur;
+    }
+    uint32_t nw[kTop];
+    const int slot0 = (head + cnt) & (kRing - 1);
+#pragma unroll
+    for (int k = 0; k < kTop; ++k) {
+      nw[k] = twist(cur, nx[k], far[k]);
+      ring[((slot0 + k) & (kRing - 1)) * 64] = temper(cur);
       cur = nx[k];
     }
-    p += kTop;
-    p -= p >= kMtN ? kMtN : 0;
+    uint4* o4 = reinterpret_cast<uint4*>(mt) + p / 4;
+    o4[0] = make_uint4(nw[0], nw[1], nw[2], nw[3]);
+    o4[1] = make_uint4(nw[4], nw[5], nw[6], nw[7]);
+    o4[2] = make_uint4(nw[8], nw[9], nw[10], nw[11]);
+    o4[3] = make_uint4(nw[12], nw[13], nw[14], nw[15]);
+    p = pn;
     cnt += kTop;
   }
   __device__ void top_up_if_low() {
-    if (__any(cnt < kLow) && cnt <= kRing - kTop) top_up();
+    if (__any(cnt < kLow) && cnt <= kRing - kTop && (p & (kTop - 1)) == 0) top_up();
   }
-  // one draw straight from the stream (ring empty: a long rejection streak, rare)
+  // one draw straight from the stream (ring empty: before the first aligned block,
+  // or a long rejection streak)
   __device__ uint32_t gen_direct() {
     int i1 = p + 1, i2 = p + kMtM;
     i1 -= i1 >= kMtN ? kMtN : 0;
@@ -182,7 +209,7 @@ struct NpStream {
   }
   __device__ uint32_t next() {
     if (cnt == 0) return gen_direct();
-    const uint32_t v = ring[head];
+    const uint32_t v = ring[head * 64];
     head = (head + 1) & (kRing - 1);
     --cnt;
     return v;
@@ -193,7 +220,7 @@ struct NpStream {
     for (int j = 0; j < cnt; ++j) {  // rewind the unconsumed tail
       int pos = q + j;
       pos -= pos >= kMtN ? kMtN : 0;
-      mt[pos] = untemper(ring[(head + j) & (kRing - 1)]);
+      mt[pos] = untemper(ring[((head + j) & (kRing - 1)) * 64]);
       if (pos == 0) mt[kMtN + 1] = saved_prev;
     }
     mt[kMtN] = (uint32_t)q;
@@ -293,7 +320,7 @@ struct GCells {
 // explored << 5 | code << 6.  A field of 31 means "31 or more": the exact count is
 // the clone's word (cellw) or, once this simulation has bumped the cell, csim
 // (valid where csg holds the simulation's stamp).  Undo = copy the clone's pristine
-// bytes (cellb, global, 16-B loads) back over the lane's LDS cells.
+// bytes (cellb, global, 16-B loads) back over the lane's LDS cells.  cb is 4-B aligned.
 constexpr uint32_t kLSat = 31u, kLExpl = 32u;
 constexpr int kLCodeShift = 6;
 
@@ -303,12 +330,12 @@ __device__ __forceinline__ uint32_t sat_byte(uint32_t w) {
 }
 
 struct LCells {
-  uint8_t* cb;            // this lane's cells (LDS, 16-B aligned)
+  uint8_t* cb;            // this lane's cells (LDS)
   const uint4* pristine;  // this lane's clone bytes (global)
   const uint32_t* cw;     // exact clone words (global)
   uint32_t* csim;         // exact sim counts of bumped saturated cells (global)
   uint32_t* csg;          // their stamps
-  int G, c, nchunk;       // nchunk = padded cells / 16
+  int G, c, nchunk, ldsw; // nchunk = pristine 16-B chunks, ldsw = LDS dwords per lane
   uint32_t stamp;
   uint32_t b[5];
   __device__ uint32_t exact(int i) const { return csg[i] == stamp ? csim[i] : (cw[i] & kVisMask); }
@@ -344,9 +371,15 @@ struct LCells {
     cb[c] = (uint8_t)((b[4] & ~(3u << kLCodeShift)) | ((uint32_t)HYD << kLCodeShift));
   }
   __device__ void undo() {
-    uint4* dst = reinterpret_cast<uint4*>(cb);
+    uint32_t* d = reinterpret_cast<uint32_t*>(cb);
 #pragma unroll 8
-    for (int k = 0; k < nchunk; ++k) dst[k] = pristine[k];  // LDS stores never alias the loads
+    for (int k = 0; k < nchunk; ++k) {  // LDS stores never alias the loads
+      const uint4 v = pristine[k];
+      if (4 * k + 0 < ldsw) d[4 * k + 0] = v.x;
+      if (4 * k + 1 < ldsw) d[4 * k + 1] = v.y;
+      if (4 * k + 2 < ldsw) d[4 * k + 2] = v.z;
+      if (4 * k + 3 < ldsw) d[4 * k + 3] = v.w;
+    }
     ++stamp;
   }
 };
@@ -634,36 +667,45 @@ __global__ __launch_bounds__(64) void pe_mcts_search_kernel(MctsArgs a) {
   cs.lg = a.ulog + e * (int64_t)(a.max_depth + 4);
   cs.nlog = 0;
   cs.G = a.g.G;
-  search_env(a, e, cs, ring + threadIdx.x * kRing);
+  search_env(a, e, cs, ring + threadIdx.x);
 }
 
-// G <= 64: the workgroup's 64 sim envs live in LDS (lane-private regions): the
-// rollout's neighbour reads and updates never leave the CU.
+// G <= 64: the workgroup's 64 sim envs live in LDS (lane-private regions with an
+// odd dword stride, so lanes at the same cell hit different banks): the rollout's
+// neighbour reads and updates never leave the CU.
 __global__ __launch_bounds__(64) void pe_mcts_search_lds_kernel(MctsArgs a) {
   extern __shared__ __align__(16) uint8_t lds[];
   const int lane = threadIdx.x;
   const int64_t e0 = (int64_t)blockIdx.x * 64;
-  const int ggp = a.ggp;
+  const int ggp = a.ggp, ldsw = a.ldsp / 4, nchunk = ggp / 16;
   // cooperative copy of the 64 clones (coalesced 16-B reads)
-  const int nchunk = ggp / 16;
-  const int64_t lim = ((int64_t)a.n - e0 < 64 ? (int64_t)a.n - e0 : 64) * nchunk;
+  const int64_t nenv = (int64_t)a.n - e0 < 64 ? (int64_t)a.n - e0 : 64;
   const uint4* src = reinterpret_cast<const uint4*>(a.cellb + e0 * ggp);
-  uint4* dst = reinterpret_cast<uint4*>(lds);
-  for (int64_t i = lane; i < lim; i += 64) dst[i] = src[i];
+  uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
+  for (int64_t i = lane; i < nenv * nchunk; i += 64) {
+    const int el = (int)(i / nchunk), k = (int)(i - (int64_t)el * nchunk);
+    const uint4 v = src[i];
+    uint32_t* d = l32 + el * ldsw + 4 * k;
+    if (4 * k + 0 < ldsw) d[0] = v.x;
+    if (4 * k + 1 < ldsw) d[1] = v.y;
+    if (4 * k + 2 < ldsw) d[2] = v.z;
+    if (4 * k + 3 < ldsw) d[3] = v.w;
+  }
   __syncthreads();
   const int64_t e = e0 + lane;
   if (e >= a.n) return;
   if (a.mask && !a.mask[e]) return;
   LCells cs;
-  cs.cb = lds + lane * ggp;
+  cs.cb = lds + lane * a.ldsp;
   cs.pristine = reinterpret_cast<const uint4*>(a.cellb + e * ggp);
   cs.cw = a.cellw + e * (int64_t)a.g.GG;
   cs.csim = a.csim + e * (int64_t)a.g.GG;
   cs.csg = a.csg + e * (int64_t)a.g.GG;
   cs.G = a.g.G;
   cs.nchunk = nchunk;
+  cs.ldsw = ldsw;
   cs.stamp = 1;
-  search_env(a, e, cs, reinterpret_cast<uint32_t*>(lds + 64 * ggp) + lane * kRing);
+  search_env(a, e, cs, reinterpret_cast<uint32_t*>(lds + 64 * a.ldsp) + lane);
 }
 
 // np.random.seed(seed) (init_genrand, pos 624) then the pending block twist, giving
@@ -920,13 +962,16 @@ int pe_mcts_search(pe_mcts* m, const uint8_t* mask, int32_t* actions, int32_t* r
   a.rvalue = root_value;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t cells = (int64_t)h->n * h->g.GG;
-  const size_t lds = 64 * ((size_t)m->ggp + 4 * (size_t)kRing);
+  int ldsp = (h->g.GG + 3) / 4 * 4;
+  if ((ldsp / 4) % 2 == 0) ldsp += 4;  // odd dword stride between lanes
+  const size_t lds = 64 * ((size_t)ldsp + 4 * (size_t)kRing);
   const bool use_lds = h->g.G <= 64 && lds <= kMctsLdsMax && !m->force_global;
   if (use_lds) {
     a.cellb = m->cellb;
     a.csim = m->csim;
     a.csg = m->csg;
     a.ggp = m->ggp;
+    a.ldsp = ldsp;
   }
   if (cells > 0) {
     hipLaunchKernelGGL(pe_mcts_clone_kernel, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, a);
