@@ -87,8 +87,13 @@ typedef struct pe_config {
     double r_step, r_exploration, r_revisit, r_complete; /* plantos_env.py:80-83 */
     uint64_t seed;              /* device-rng key (Philox4x32-10)               */
     uint32_t env_id_offset;     /* global id of env 0 (sharding across GPUs)    */
-    int32_t reserved[7];
+    int32_t map_generation_algo; /* PE_MAP_ORIGINAL (0, plantos_env.py:338-372) or
+                                    PE_MAP_MAZE (the fork's map_generation_algo='maze',
+                                    gradio-app/plantos_env_new.py:355-358, 408-604; G >= 7) */
+    int32_t reserved[6];
 } pe_config;
+
+enum pe_map_algo { PE_MAP_ORIGINAL = 0, PE_MAP_MAZE = 1 };
 
 typedef struct pe_handle pe_handle;
 

@@ -27,6 +27,7 @@ class POConfig(ctypes.Structure):
         ("r_goal", ctypes.c_double), ("r_mistake", ctypes.c_double), ("r_invalid", ctypes.c_double),
         ("r_water_empty", ctypes.c_double), ("r_step", ctypes.c_double), ("r_exploration", ctypes.c_double),
         ("r_revisit", ctypes.c_double), ("r_complete", ctypes.c_double),
+        ("map_algo", ctypes.c_int32), ("pad_", ctypes.c_int32),
     ]
 
 

@@ -37,6 +37,7 @@ void po_default_config(po_config* c, int G, int P, int O, int R, int C) {
     c->r_exploration = 10;
     c->r_revisit = -1;
     c->r_complete = 50;
+    c->map_algo = 0;
 }
 
 /* plantos_env.py:55-57: lidar_channels*5 + 2 + 25 */
@@ -598,11 +599,10 @@ int po_pyset_free_list(int G, const uint8_t* obstacle_mask, int32_t* out) {
 }
 
 /* ================================================================ map generation */
-/* _generate_map, plantos_env.py:338-372; `cpython` selects list order + sample algorithm. */
-static int generate_map(const po_config* c, u32src* src, int cpython, uint8_t* cells, int* rx, int* ry) {
-    const int G = c->grid_size, P = c->num_plants;
-    const int GG = G * G;
-    uint8_t* obst = (uint8_t*)calloc((size_t)GG, 1);
+/* Obstacle clusters of _generate_map(_original), plantos_env.py:341-354. */
+static void clusters_original(const po_config* c, u32src* src, uint8_t* obst) {
+    const int G = c->grid_size;
+    memset(obst, 0, (size_t)(G * G));
     const int clusters = c->num_obstacles / 3;                     /* :341 */
     for (int q = 0; q < clusters; ++q) {                           /* :343 */
         int cx = 2 + (int)randbelow(src, (uint32_t)(G - 4));       /* randint(2, G-3) :344 */
@@ -613,6 +613,119 @@ static int generate_map(const po_config* c, u32src* src, int cpython, uint8_t* c
                 int ox = cx + dx - size / 2, oy = cy + dy - size / 2; /* :350-351 */
                 if (0 <= ox && ox < G && 0 <= oy && oy < G) obst[ox * G + oy] = 1; /* :353-354 */
             }
+    }
+}
+
+/* ---- the fork's maze, gradio-app/plantos_env_new.py:408-604 ---- */
+static void carve(uint8_t* obst, int G, int x, int y) {
+    if (0 <= x && x < G && 0 <= y && y < G) obst[x * G + y] = 0;  /* obstacles.discard */
+}
+
+/* _carve_irregular_room :482-515 */
+static void maze_room(u32src* src, uint8_t* obst, int G, int mx, int my) {
+    const int bx = mx * 6 + 1, by = my * 6 + 1;
+    for (int i = 0; i < 5; ++i)
+        for (int j = 0; j < 5; ++j) carve(obst, G, bx + i, by + j);
+    if (random53(src) < 0.3)                                       /* extend right :494-500 */
+        for (int i = 0; i < 2; ++i)
+            for (int j = 2; j < 4; ++j) carve(obst, G, bx + 5 + i, by + j);
+    if (random53(src) < 0.3)                                       /* extend down :502-508 */
+        for (int i = 2; i < 4; ++i)
+            for (int j = 0; j < 2; ++j) carve(obst, G, bx + i, by + 5 + j);
+    if (random53(src) < 0.4) {                                     /* corner cut :511-515 */
+        static const int CORNER[4][2] = {{0, 0}, {4, 0}, {0, 4}, {4, 4}};
+        const int k = (int)randbelow(src, 4u);                     /* random.choice(corners) */
+        const int x = bx + CORNER[k][0], y = by + CORNER[k][1];
+        if (0 <= x && x < G && 0 <= y && y < G) obst[x * G + y] = 1;  /* obstacles.add */
+    }
+}
+
+/* _carve_straight_path :537-555 (width 5) */
+static void maze_straight(uint8_t* obst, int G, int cx, int cy, int nx, int ny) {
+    if (cx == nx) {
+        const int lo = cy < ny ? cy : ny, hi = cy < ny ? ny : cy;
+        for (int m = lo; m <= hi; ++m)
+            for (int i = 0; i < 5; ++i)
+                for (int j = 0; j < 6; ++j) carve(obst, G, cx * 6 + 1 + i, m * 6 + 1 + j);
+    } else {
+        const int lo = cx < nx ? cx : nx, hi = cx < nx ? nx : cx;
+        for (int m = lo; m <= hi; ++m)
+            for (int i = 0; i < 6; ++i)
+                for (int j = 0; j < 5; ++j) carve(obst, G, m * 6 + 1 + i, cy * 6 + 1 + j);
+    }
+}
+
+/* _carve_irregular_path :517-535 (cardinal moves only) + _add_path_bulge :557-580 */
+static void maze_path(u32src* src, uint8_t* obst, int G, int cx, int cy, int nx, int ny, int dx) {
+    maze_straight(obst, G, cx, cy, nx, ny);
+    if (random53(src) < 0.2) {
+        const int mx = (cx + nx) / 2, my = (cy + ny) / 2;
+        const int dir = randbelow(src, 2u) ? 1 : -1;               /* random.choice([-1, 1]) */
+        for (int i = 0; i < 2; ++i)
+            for (int j = 0; j < 2; ++j) {
+                if (dx == 0)
+                    carve(obst, G, mx * 6 + 2 + dir * 2 + i, my * 6 + 2 + j);
+                else
+                    carve(obst, G, mx * 6 + 2 + i, my * 6 + 2 + dir * 2 + j);
+            }
+    }
+}
+
+/* _generate_map_maze :408-480 up to the plant placement.  Returns -1 when the meta grid
+ * is empty (G < 7: random.randint(0, -1) raises ValueError). */
+static int maze_obstacles(u32src* src, uint8_t* obst, int G) {
+    static const int DIRS[4][2] = {{0, 1}, {0, -1}, {1, 0}, {-1, 0}};
+    memset(obst, 1, (size_t)(G * G));                              /* grid full of obstacles :413 */
+    const int mw = (G - 1) / 6;                                    /* meta_w == meta_h :417-418 */
+    if (mw < 1) return -1;
+    uint8_t* visited = (uint8_t*)calloc((size_t)(mw * mw), 1);
+    int* stack = (int*)malloc(sizeof(int) * (size_t)(mw * mw));
+    int sp = 0;
+    const int sx = (int)randbelow(src, (uint32_t)mw);              /* randint(0, meta_w - 1) :427 */
+    const int sy = (int)randbelow(src, (uint32_t)mw);
+    stack[sp++] = sx * mw + sy;
+    visited[sx * mw + sy] = 1;
+    maze_room(src, obst, G, sx, sy);                               /* :432 */
+    while (sp > 0) {                                               /* randomized DFS :435-456 */
+        const int cx = stack[sp - 1] / mw, cy = stack[sp - 1] % mw;
+        int cand[4], nc = 0;
+        for (int d = 0; d < 4; ++d) {
+            const int nx = cx + DIRS[d][0], ny = cy + DIRS[d][1];
+            if (0 <= nx && nx < mw && 0 <= ny && ny < mw && !visited[nx * mw + ny]) cand[nc++] = d;
+        }
+        if (nc) {
+            const int d = cand[randbelow(src, (uint32_t)nc)];     /* random.choice(neighbors) */
+            const int nx = cx + DIRS[d][0], ny = cy + DIRS[d][1];
+            maze_path(src, obst, G, cx, cy, nx, ny, DIRS[d][0]);
+            maze_room(src, obst, G, nx, ny);
+            visited[nx * mw + ny] = 1;
+            stack[sp++] = nx * mw + ny;
+        } else {
+            --sp;
+        }
+    }
+    free(visited);
+    free(stack);
+    return 0;
+}
+
+/* _generate_map: 'original' (plantos_env.py:338-372) or the fork's 'maze' (falls back to
+ * the original generator, same stream, when the maze has no room, :461-465).
+ * `cpython` selects list order + sample algorithm. */
+static int generate_map(const po_config* c, u32src* src, int cpython, uint8_t* cells, int* rx, int* ry) {
+    const int G = c->grid_size, P = c->num_plants;
+    const int GG = G * G;
+    uint8_t* obst = (uint8_t*)calloc((size_t)GG, 1);
+    if (c->map_algo == 1) {
+        if (maze_obstacles(src, obst, G) != 0) {
+            free(obst);
+            return -1;
+        }
+        int nfree = 0;
+        for (int k = 0; k < GG; ++k) nfree += !obst[k];
+        if (nfree < P + 1) clusters_original(c, src, obst);   /* "Falling back to original" */
+    } else {
+        clusters_original(c, src, obst);
     }
     int32_t* list = (int32_t*)malloc(sizeof(int32_t) * (size_t)GG);
     pyset avail;

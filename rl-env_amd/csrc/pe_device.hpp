@@ -101,6 +101,7 @@ struct Rules {
   int P, O, max_steps;
   double cur_max, cur_inc;  // CurriculumWrapper max_threshold, threshold_increment
   int cur_max_eps;          // max_episodes_per_maze (A2C_training.py:54)
+  int map_algo;             // PE_MAP_ORIGINAL / PE_MAP_MAZE (the fork, plantos_env_new.py:355-358)
 };
 
 // CurriculumWrapper.step (A2C_training.py:97-109): exploration_percentage >= the
@@ -348,19 +349,11 @@ __device__ inline int img_nth_cell(const uint64_t* sg, const Geo& g, const Table
   return 0;  // unreachable when j < count
 }
 
-// _generate_map (plantos_env.py:338-372) in the device-rng mode defined by
-// oracle po_reset_philox: Philox stream keyed by (seed, global env id, episode),
-// candidate lists in row-major order.  Writes the grid image sg (all rows) and
-// returns the new scalars of the episode (flags F_NOROOM if there is no room,
-// plantos_env.py:360-364).  picks: P u16 of scratch.
-__device__ inline Scal gen_map(const Geo& g, const Rules& rl, const Tables* tab, uint64_t* sg, uint16_t* picks,
-                               uint32_t env_id, uint32_t episode) {
+// Obstacle clusters of _generate_map (plantos_env.py:341-354) on an empty image.
+__device__ inline void clusters_original(const Geo& g, const Rules& rl, const Tables* tab, uint64_t* sg, Stream& rng) {
   const int G = g.G;
   for (int row = 0; row < G; ++row)
     for (int w = 0; w < g.WPR; ++w) sg[row * g.WPR + w] = tab->grid_pad[w];
-  Stream rng;
-  rng.init(rl.seed, env_id, episode);
-  // obstacle clusters, plantos_env.py:341-354
   const int clusters = rl.O / 3;
   for (int q = 0; q < clusters; ++q) {
     const int cx = 2 + (int)rng.below((uint32_t)(G - 4));
@@ -371,6 +364,122 @@ __device__ inline Scal gen_map(const Geo& g, const Rules& rl, const Tables* tab,
         const int ox = cx + dx - size / 2, oy = cy + dy - size / 2;
         if (0 <= ox && ox < G && 0 <= oy && oy < G) img_set(sg, g, ox, oy + g.R, OBST);
       }
+  }
+}
+
+// ---- the fork's maze (gradio-app/plantos_env_new.py:408-604) on a grid image.
+__device__ __forceinline__ void img_carve(uint64_t* sg, const Geo& g, int x, int y) {
+  if (0 <= x && x < g.G && 0 <= y && y < g.G) img_set(sg, g, x, y + g.R, EMPTY);  // obstacles.discard
+}
+
+// _carve_irregular_room (:479-516)
+__device__ inline void maze_room(const Geo& g, uint64_t* sg, Stream& rng, int mx, int my) {
+  const int bx = mx * 6 + 1, by = my * 6 + 1;
+  for (int i = 0; i < 5; ++i)
+    for (int j = 0; j < 5; ++j) img_carve(sg, g, bx + i, by + j);
+  if (rng.random53() < 0.3)  // extend right
+    for (int i = 0; i < 2; ++i)
+      for (int j = 2; j < 4; ++j) img_carve(sg, g, bx + 5 + i, by + j);
+  if (rng.random53() < 0.3)  // extend down
+    for (int i = 2; i < 4; ++i)
+      for (int j = 0; j < 2; ++j) img_carve(sg, g, bx + i, by + 5 + j);
+  if (rng.random53() < 0.4) {  // corner cut: random.choice([(0,0), (4,0), (0,4), (4,4)])
+    const int k = (int)rng.below(4u);
+    const int x = bx + ((k & 1) ? 4 : 0), y = by + ((k & 2) ? 4 : 0);
+    if (x < g.G && y < g.G) img_set(sg, g, x, y + g.R, OBST);  // obstacles.add
+  }
+}
+
+// _carve_irregular_path (:518-536, cardinal moves) = _carve_straight_path (:538-557,
+// width 5) + a 20 % path bulge (_add_path_bulge :559-582)
+__device__ inline void maze_path(const Geo& g, uint64_t* sg, Stream& rng, int cx, int cy, int nx, int ny) {
+  if (cx == nx) {
+    const int lo = cy < ny ? cy : ny, hi = cy < ny ? ny : cy;
+    for (int m = lo; m <= hi; ++m)
+      for (int i = 0; i < 5; ++i)
+        for (int j = 0; j < 6; ++j) img_carve(sg, g, cx * 6 + 1 + i, m * 6 + 1 + j);
+  } else {
+    const int lo = cx < nx ? cx : nx, hi = cx < nx ? nx : cx;
+    for (int m = lo; m <= hi; ++m)
+      for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 5; ++j) img_carve(sg, g, m * 6 + 1 + i, cy * 6 + 1 + j);
+  }
+  if (rng.random53() < 0.2) {
+    const int mx = (cx + nx) / 2, my = (cy + ny) / 2;
+    const int dir = rng.below(2u) ? 1 : -1;  // random.choice([-1, 1])
+    for (int i = 0; i < 2; ++i)
+      for (int j = 0; j < 2; ++j) {
+        if (cx == nx)  // dx == 0: vertical path, horizontal bulge
+          img_carve(sg, g, mx * 6 + 2 + dir * 2 + i, my * 6 + 2 + j);
+        else
+          img_carve(sg, g, mx * 6 + 2 + i, my * 6 + 2 + dir * 2 + j);
+      }
+  }
+}
+
+// Maze obstacles (:408-456): all cells obstacles, randomized DFS over the
+// (G-1)/6 meta grid carving rooms and paths.  G >= 7 (pe_create checks).  A meta
+// cell is visited iff its centre (6a+3, 6b+3) is carved: rooms always carve it and
+// nothing else ever touches a centre (paths carve only between visited cells,
+// bulges/extensions/corners sit at other residues mod 6), so no visited map is
+// kept; the DFS stack is the chain of parent directions (2 bits per meta cell in
+// `par`, maze_scratch_bytes).
+__device__ inline void maze_obstacles(const Geo& g, const Tables* tab, uint64_t* sg, uint8_t* par, Stream& rng) {
+  const int G = g.G, mw = (G - 1) / 6;
+  for (int row = 0; row < G; ++row)
+    for (int w = 0; w < g.WPR; ++w) sg[row * g.WPR + w] = tab->grid_pad[w] | tab->grid_real[w];
+  const int sx = (int)rng.below((uint32_t)mw), sy = (int)rng.below((uint32_t)mw);  // randint(0, meta_w-1)
+  maze_room(g, sg, rng, sx, sy);
+  int cx = sx, cy = sy;
+  for (;;) {
+    int cand[4], nc = 0;
+    // (0,1), (0,-1), (1,0), (-1,0) (:440)
+    if (cy + 1 < mw && img_code(sg, g, cx * 6 + 3, (cy + 1) * 6 + 3 + g.R) == OBST) cand[nc++] = 0;
+    if (cy > 0 && img_code(sg, g, cx * 6 + 3, (cy - 1) * 6 + 3 + g.R) == OBST) cand[nc++] = 1;
+    if (cx + 1 < mw && img_code(sg, g, (cx + 1) * 6 + 3, cy * 6 + 3 + g.R) == OBST) cand[nc++] = 2;
+    if (cx > 0 && img_code(sg, g, (cx - 1) * 6 + 3, cy * 6 + 3 + g.R) == OBST) cand[nc++] = 3;
+    if (nc) {
+      const uint32_t r = rng.below((uint32_t)nc);
+      const int d = r == 0 ? cand[0] : (r == 1 ? cand[1] : (r == 2 ? cand[2] : cand[3]));
+      const int nx = cx + (d == 2 ? 1 : (d == 3 ? -1 : 0)), ny = cy + (d == 0 ? 1 : (d == 1 ? -1 : 0));
+      maze_path(g, sg, rng, cx, cy, nx, ny);
+      maze_room(g, sg, rng, nx, ny);
+      const int m = nx * mw + ny;
+      par[m >> 2] = (uint8_t)((par[m >> 2] & ~(3u << (2 * (m & 3)))) | ((uint32_t)d << (2 * (m & 3))));
+      cx = nx;
+      cy = ny;
+    } else {
+      if (cx == sx && cy == sy) break;  // stack empty
+      const int m = cx * mw + cy;
+      const int d = (par[m >> 2] >> (2 * (m & 3))) & 3;  // pop: back to the parent
+      cx -= d == 2 ? 1 : (d == 3 ? -1 : 0);
+      cy -= d == 0 ? 1 : (d == 1 ? -1 : 0);
+    }
+  }
+}
+
+// _generate_map (plantos_env.py:338-372; the fork's 'maze' :355-358, 408-477) in the
+// device-rng mode defined by oracle po_reset_philox: Philox stream keyed by (seed,
+// global env id, episode), candidate lists in row-major order.  Writes the grid
+// image sg (all rows) and returns the new scalars of the episode (flags F_NOROOM
+// if there is no room, plantos_env.py:360-364).  picks: max(2P,
+// maze_scratch_bytes(G)) bytes of scratch.
+__device__ inline Scal gen_map(const Geo& g, const Rules& rl, const Tables* tab, uint64_t* sg, uint16_t* picks,
+                               uint32_t env_id, uint32_t episode) {
+  const int G = g.G;
+  Stream rng;
+  rng.init(rl.seed, env_id, episode);
+  if (rl.map_algo == 1) {
+    maze_obstacles(g, tab, sg, reinterpret_cast<uint8_t*>(picks), rng);
+    int nfree = 0;
+    for (int row = 0; row < G; ++row)
+      for (int w = 0; w < g.WPR; ++w) {
+        const uint64_t v = sg[row * g.WPR + w];
+        nfree += __popcll(~v & tab->grid_real[w]);  // real cells whose code has the low bit clear
+      }
+    if (nfree < rl.P + 1) clusters_original(g, rl, tab, sg, rng);  // fallback, same stream (:461-466)
+  } else {
+    clusters_original(g, rl, tab, sg, rng);
   }
   int n_obst = 0;
   for (int row = 0; row < G; ++row)
@@ -456,8 +565,13 @@ __device__ inline Scal reset_env(const State& st, const Geo& g, const Rules& rl,
   return s;
 }
 
-// Bytes of LDS scratch reset_env_scratch needs (grid image + picks, 8-B aligned).
-__host__ __device__ constexpr int reset_scratch_bytes(int G, int WPR, int P) { return 8 + G * WPR * 8 + 2 * P; }
+// Scratch of the maze DFS: 2 bits per meta cell.
+__host__ __device__ constexpr int maze_scratch_bytes(int G) { return (((G - 1) / 6) * ((G - 1) / 6) + 3) / 4; }
+
+// Bytes of LDS scratch reset_env_scratch needs (grid image + picks/maze DFS, 8-B aligned).
+__host__ __device__ constexpr int reset_scratch_bytes(int G, int WPR, int P) {
+  return 8 + G * WPR * 8 + (2 * P > maze_scratch_bytes(G) ? 2 * P : maze_scratch_bytes(G));
+}
 
 // reset() generated in a scratch image (LDS) and written to HBM row by row:
 // the rejection-sampling scans run at LDS latency instead of HBM latency.

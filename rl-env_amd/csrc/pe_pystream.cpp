@@ -18,6 +18,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <new>
 #include <string>
@@ -236,6 +237,7 @@ struct PySet {
 
 struct pe_pystream {
   int G, P, O;
+  bool maze;         // map_generation_algo == 'maze' (the fork, plantos_env_new.py:355-358)
   double p_thirsty;
   Mt mt;
   PySet full;        // set((x, y) for x in range(G) for y in range(G)), fixed per G
@@ -254,9 +256,9 @@ int sample_setsize(int k) {
   return setsize;
 }
 
-// _generate_map for one env: cells u8[G*G] (pe_cell codes), rover (x, y).
-int gen_one(pe_pystream* s, uint8_t* cells, int32_t* rover) {
-  const int G = s->G, GG = G * G, P = s->P;
+// Obstacle clusters of _generate_map(_original), plantos_env.py:341-354; returns len(obstacles).
+int clusters_original(pe_pystream* s) {
+  const int G = s->G;
   Mt& mt = s->mt;
   std::fill(s->obst.begin(), s->obst.end(), 0);
   int n_obst = 0;
@@ -272,6 +274,101 @@ int gen_one(pe_pystream* s, uint8_t* cells, int32_t* rover) {
           ++n_obst;
         }
       }
+  }
+  return n_obst;
+}
+
+// ---- the fork's maze, gradio-app/plantos_env_new.py:408-604 (obstacles only)
+void carve(pe_pystream* s, int x, int y) {
+  if (0 <= x && x < s->G && 0 <= y && y < s->G) s->obst[x * s->G + y] = 0;  // obstacles.discard
+}
+
+void maze_room(pe_pystream* s, int mx, int my) {                    // _carve_irregular_room :479-516
+  Mt& mt = s->mt;
+  const int bx = mx * 6 + 1, by = my * 6 + 1;
+  for (int i = 0; i < 5; ++i)
+    for (int j = 0; j < 5; ++j) carve(s, bx + i, by + j);
+  if (mt.random() < 0.3)
+    for (int i = 0; i < 2; ++i)
+      for (int j = 2; j < 4; ++j) carve(s, bx + 5 + i, by + j);
+  if (mt.random() < 0.3)
+    for (int i = 2; i < 4; ++i)
+      for (int j = 0; j < 2; ++j) carve(s, bx + i, by + 5 + j);
+  if (mt.random() < 0.4) {
+    static const int CORNER[4][2] = {{0, 0}, {4, 0}, {0, 4}, {4, 4}};
+    const int k = (int)mt.below(4u);                                // random.choice(corners)
+    const int x = bx + CORNER[k][0], y = by + CORNER[k][1];
+    if (x < s->G && y < s->G) s->obst[x * s->G + y] = 1;             // obstacles.add
+  }
+}
+
+void maze_path(pe_pystream* s, int cx, int cy, int nx, int ny) {    // :518-582
+  if (cx == nx) {
+    for (int m = std::min(cy, ny); m <= std::max(cy, ny); ++m)
+      for (int i = 0; i < 5; ++i)
+        for (int j = 0; j < 6; ++j) carve(s, cx * 6 + 1 + i, m * 6 + 1 + j);
+  } else {
+    for (int m = std::min(cx, nx); m <= std::max(cx, nx); ++m)
+      for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 5; ++j) carve(s, m * 6 + 1 + i, cy * 6 + 1 + j);
+  }
+  if (s->mt.random() < 0.2) {                                       // _add_path_bulge
+    const int mx = (cx + nx) / 2, my = (cy + ny) / 2;
+    const int dir = s->mt.below(2u) ? 1 : -1;                       // random.choice([-1, 1])
+    for (int i = 0; i < 2; ++i)
+      for (int j = 0; j < 2; ++j) {
+        if (cx == nx)
+          carve(s, mx * 6 + 2 + dir * 2 + i, my * 6 + 2 + j);
+        else
+          carve(s, mx * 6 + 2 + i, my * 6 + 2 + dir * 2 + j);
+      }
+  }
+}
+
+// _generate_map_maze up to the plants (:408-456); returns len(obstacles).
+int maze_obstacles(pe_pystream* s) {
+  static const int DIRS[4][2] = {{0, 1}, {0, -1}, {1, 0}, {-1, 0}};
+  const int G = s->G, mw = (G - 1) / 6;
+  std::fill(s->obst.begin(), s->obst.end(), 1);
+  std::vector<uint8_t> visited((size_t)mw * mw, 0);
+  std::vector<int> stack;
+  const int sx = (int)s->mt.below((uint32_t)mw), sy = (int)s->mt.below((uint32_t)mw);  // randint(0, meta-1)
+  stack.push_back(sx * mw + sy);
+  visited[sx * mw + sy] = 1;
+  maze_room(s, sx, sy);
+  while (!stack.empty()) {
+    const int cx = stack.back() / mw, cy = stack.back() % mw;
+    int cand[4], nc = 0;
+    for (int d = 0; d < 4; ++d) {
+      const int nx = cx + DIRS[d][0], ny = cy + DIRS[d][1];
+      if (0 <= nx && nx < mw && 0 <= ny && ny < mw && !visited[nx * mw + ny]) cand[nc++] = d;
+    }
+    if (nc) {
+      const int d = cand[s->mt.below((uint32_t)nc)];               // random.choice(neighbors)
+      const int nx = cx + DIRS[d][0], ny = cy + DIRS[d][1];
+      maze_path(s, cx, cy, nx, ny);
+      maze_room(s, nx, ny);
+      visited[nx * mw + ny] = 1;
+      stack.push_back(nx * mw + ny);
+    } else {
+      stack.pop_back();
+    }
+  }
+  int n = 0;
+  for (uint8_t v : s->obst) n += v;
+  return n;
+}
+
+// _generate_map for one env: cells u8[G*G] (pe_cell codes), rover (x, y).
+int gen_one(pe_pystream* s, uint8_t* cells, int32_t* rover) {
+  const int G = s->G, GG = G * G, P = s->P;
+  Mt& mt = s->mt;
+  int n_obst;
+  if (s->maze) {
+    n_obst = maze_obstacles(s);
+    if (GG - n_obst < P + 1) n_obst = clusters_original(s);        // fallback, same stream (:461-466)
+  } else {
+    n_obst = clusters_original(s);
   }
   // available_positions = set(all) - obstacles   (:356-358, set_difference)
   PySet avail;
@@ -332,11 +429,15 @@ int pe_pystream_create(const pe_config* c, int64_t seed, pe_pystream** out) {
     return pe_internal_set_error(PE_ERR_ARG, "randint(2, G-3) needs grid_size >= 5 (plantos_env.py:344)");
   if (G < 1 || G > 128 || c->num_plants < 0 || c->num_obstacles < 0)
     return pe_internal_set_error(PE_ERR_ARG, "bad geometry");
+  if (c->map_generation_algo == PE_MAP_MAZE && G < 7)
+    return pe_internal_set_error(PE_ERR_ARG, "the maze needs grid_size >= 7 (randint(0, (G-1)//6 - 1), "
+                                             "plantos_env_new.py:427)");
   pe_pystream* s = new (std::nothrow) pe_pystream();
   if (!s) return pe_internal_set_error(PE_ERR_NOMEM, "host allocation failed");
   s->G = G;
   s->P = c->num_plants;
   s->O = c->num_obstacles;
+  s->maze = c->map_generation_algo == PE_MAP_MAZE;
   s->p_thirsty = c->thirsty_plant_prob;
   s->mt.seed(seed < 0 ? (uint64_t)(-(seed + 1)) + 1u : (uint64_t)seed);  // random.seed: abs(a)
   s->cell_hash.resize((size_t)G * G);

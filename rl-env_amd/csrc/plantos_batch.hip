@@ -1287,6 +1287,10 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   if (O < 0) return fail(PE_ERR_ARG, "num_obstacles must be >= 0");
   if (O / 3 > 0 && G < 5) return fail(PE_ERR_ARG, "randint(2, G-3) needs grid_size >= 5 (plantos_env.py:344)");
   if (c->max_steps < 1 || c->max_steps > 65535) return fail(PE_ERR_ARG, "max_steps must be in [1, 65535]");
+  if (c->map_generation_algo != PE_MAP_ORIGINAL && c->map_generation_algo != PE_MAP_MAZE)
+    return fail(PE_ERR_ARG, "map_generation_algo must be PE_MAP_ORIGINAL or PE_MAP_MAZE");
+  if (c->map_generation_algo == PE_MAP_MAZE && G < 7)
+    return fail(PE_ERR_ARG, "the maze needs grid_size >= 7 (randint(0, (G-1)//6 - 1), plantos_env_new.py:427)");
   if (n_envs < 1) return fail(PE_ERR_ARG, "n_envs must be >= 1");
   if (2 * (G + 2 * R) > 64 * kMaxWPR) return fail(PE_ERR_ARG, "G + 2R too large");
 
@@ -1347,6 +1351,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   rl.env_off = c->env_id_offset;
   rl.P = P;
   rl.O = O;
+  rl.map_algo = c->map_generation_algo;
   rl.max_steps = c->max_steps;
 
   // host tables

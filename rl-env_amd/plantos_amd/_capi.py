@@ -23,6 +23,14 @@ PE_NINFO = 11
  PE_I_TOTAL_CELLS, PE_I_COLLIDED, PE_I_COLLISIONS, PE_I_POISONED) = range(11)
 
 PE_CELL_EMPTY, PE_CELL_OBSTACLE, PE_CELL_HYDRATED, PE_CELL_THIRSTY = range(4)
+PE_MAP_ORIGINAL, PE_MAP_MAZE = 0, 1
+MAP_ALGOS = {"original": PE_MAP_ORIGINAL, "maze": PE_MAP_MAZE}
+
+
+def map_algo_id(name):
+    """map_generation_algo of the fork's constructor (plantos_env_new.py:28, 355-358):
+    'maze' selects the maze; anything else is 'original', as there."""
+    return PE_MAP_MAZE if name == "maze" else PE_MAP_ORIGINAL
 
 # exported symbols (tests/test_capi_symbols.py checks they match include/plantos_batch.h)
 EXPORTS = [
@@ -43,7 +51,8 @@ class PEConfig(ctypes.Structure):
         ("r_goal", ctypes.c_double), ("r_mistake", ctypes.c_double), ("r_invalid", ctypes.c_double),
         ("r_water_empty", ctypes.c_double), ("r_step", ctypes.c_double), ("r_exploration", ctypes.c_double),
         ("r_revisit", ctypes.c_double), ("r_complete", ctypes.c_double), ("seed", ctypes.c_uint64),
-        ("env_id_offset", ctypes.c_uint32), ("reserved", ctypes.c_int32 * 7),
+        ("env_id_offset", ctypes.c_uint32), ("map_generation_algo", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 6),
     ]
 
 
@@ -136,12 +145,14 @@ class PyStream:
     """Host-side CPython `random` map stream (seed-exact reset layouts,
     plantos_env.py:338-372 after random.seed(seed)); see include/plantos_batch.h."""
 
-    def __init__(self, grid_size, num_plants, num_obstacles, seed, thirsty_plant_prob=0.7):
+    def __init__(self, grid_size, num_plants, num_obstacles, seed, thirsty_plant_prob=0.7,
+                 map_generation_algo="original"):
         import numpy as np
         self._np = np
         self.G = grid_size
         c = default_config(grid_size, num_plants, num_obstacles, 1, 1)
         c.thirsty_plant_prob = float(thirsty_plant_prob)
+        c.map_generation_algo = map_algo_id(map_generation_algo)
         h = ctypes.c_void_p()
         check(lib().pe_pystream_create(ctypes.byref(c), int(seed), ctypes.byref(h)), "pe_pystream_create")
         self._h = h

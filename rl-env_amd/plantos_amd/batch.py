@@ -19,12 +19,13 @@ class PlantOSBatch:
 
     Parameters mirror PlantOSEnv.__init__ (plantos_env.py:25-27) plus the batch
     size, device, the device-rng seed, and `env_id_offset` (global id of env 0,
-    used when the batch is one shard of a multi-GPU job).
+    used when the batch is one shard of a multi-GPU job); `map_generation_algo`
+    is the fork's ('original' or 'maze', gradio-app/plantos_env_new.py:28).
     """
 
     def __init__(self, num_envs, grid_size=21, num_plants=8, num_obstacles=50, lidar_range=2,
                  lidar_channels=10, thirsty_plant_prob=0.7, max_steps=1000, autoreset=True, seed=0,
-                 env_id_offset=0, device=None, rewards=None):
+                 env_id_offset=0, device=None, rewards=None, map_generation_algo="original"):
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device() if torch.cuda.is_available() else 0)
         self.device = torch.device(device)
@@ -37,6 +38,8 @@ class PlantOSBatch:
         cfg.autoreset = int(bool(autoreset))
         cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         cfg.env_id_offset = int(env_id_offset)
+        cfg.map_generation_algo = C.map_algo_id(map_generation_algo)
+        self.map_generation_algo = "maze" if cfg.map_generation_algo == C.PE_MAP_MAZE else "original"
         for k, v in (rewards or {}).items():
             setattr(cfg, k, float(v))
         self.cfg = cfg

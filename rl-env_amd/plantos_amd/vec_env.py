@@ -201,14 +201,16 @@ class PlantOSVecEnv(_VecEnvBase):
     def __init__(self, num_envs, grid_size=21, num_plants=8, num_obstacles=50, lidar_range=2, lidar_channels=10,
                  thirsty_plant_prob=0.7, max_steps=1000, seed=0, device=None, tensors=False, env_id_offset=0,
                  observation_mode="lidar", render_mode=None, batch=None, reset_mode="device", python_seed=None,
-                 curriculum=False):
+                 curriculum=False, map_generation_algo="original"):
         """reset_mode="device": maps from the device generator keyed by (seed, env id,
         episode) -- the throughput mode.  reset_mode="cpython": the reference's own
         layouts, seed-exact: CPython's global `random` after random.seed(python_seed)
         (default: seed), consumed in DummyVecEnv order (pe_pystream, host side).
         curriculum=True (or a dict of CurriculumWrapper arguments) applies the batched
         CurriculumWrapper of A2C_training.py:37-109 to every env, as
-        make_env_wrapper(use_curriculum=True) does (A2C_training.py:114-126)."""
+        make_env_wrapper(use_curriculum=True) does (A2C_training.py:114-126).
+        map_generation_algo="maze" selects the fork's maze layouts
+        (gradio-app/plantos_env_new.py:28, 408-604) in either reset mode."""
         if observation_mode != "lidar":
             raise ValueError("only observation_mode='lidar' exists in the reference (plantos_env.py:27)")
         if reset_mode not in ("device", "cpython"):
@@ -218,7 +220,7 @@ class PlantOSVecEnv(_VecEnvBase):
             num_envs, grid_size=grid_size, num_plants=num_plants, num_obstacles=num_obstacles,
             lidar_range=lidar_range, lidar_channels=lidar_channels, thirsty_plant_prob=thirsty_plant_prob,
             max_steps=max_steps, autoreset=reset_mode == "device", seed=seed, env_id_offset=env_id_offset,
-            device=device)
+            device=device, map_generation_algo=map_generation_algo)
         if curriculum:
             kw = dict(initial_threshold=40.0, max_threshold=100.0)  # A2C_training.py:121
             if isinstance(curriculum, dict):
@@ -228,7 +230,8 @@ class PlantOSVecEnv(_VecEnvBase):
         self._pystream = None
         if reset_mode == "cpython":
             self._pystream = C.PyStream(grid_size, num_plants, num_obstacles,
-                                        seed if python_seed is None else python_seed, thirsty_plant_prob)
+                                        seed if python_seed is None else python_seed, thirsty_plant_prob,
+                                        getattr(self.batch, "map_generation_algo", "original"))
         self.grid_size, self.num_plants, self.num_obstacles = grid_size, num_plants, num_obstacles
         self.lidar_range, self.lidar_channels = lidar_range, lidar_channels
         self.thirsty_plant_prob, self.max_steps = thirsty_plant_prob, max_steps
@@ -321,7 +324,8 @@ class PlantOSVecEnv(_VecEnvBase):
         if self.reset_mode == "cpython":  # random.seed(seed) of the reference's global stream
             self._pystream.close()
             self._pystream = C.PyStream(self.grid_size, self.num_plants, self.num_obstacles, int(seed),
-                                        self.thirsty_plant_prob)
+                                        self.thirsty_plant_prob,
+                                        getattr(self.batch, "map_generation_algo", "original"))
         return [int(seed) + i for i in range(self.num_envs)]
 
     def _indices(self, indices):

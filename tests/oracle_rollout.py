@@ -14,8 +14,8 @@ class OracleVec:
     """Device-rng (Philox) DummyVecEnv-style rollout of selected global env ids,
     mirroring pe_create (all envs reset with episode 0) + pe_step(autoreset)."""
 
-    def __init__(self, cfg_tuple, env_ids, seed, max_steps=1000):
-        self.cfg = O.config(*cfg_tuple, max_steps=max_steps)
+    def __init__(self, cfg_tuple, env_ids, seed, max_steps=1000, map_algo=0):
+        self.cfg = O.config(*cfg_tuple, max_steps=max_steps, map_algo=map_algo)
         self.ids = np.asarray(env_ids, np.int64)
         self.seed = seed
         self.b = O.Batch(self.cfg, len(self.ids))

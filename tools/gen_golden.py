@@ -591,6 +591,52 @@ def main():
     gen_curriculum("g20", 3, 2100, 13, "random")
 
 
+def gen_maze_maps(name, cfgt, seeds, resets):
+    """Consecutive reset() layouts of the fork with map_generation_algo='maze'
+    (gradio-app/plantos_env_new.py:408-604: DFS maze on a (G-1)//6 meta grid,
+    irregular rooms, path bulges; falls back to the original generator when the
+    maze has no room for the plants + rover)."""
+    G, P, O, R, C = cfgt
+    env = ForkEnv(grid_size=G, num_plants=P, num_obstacles=O, lidar_range=R, lidar_channels=C,
+                  map_generation_algo="maze")
+    cells = np.zeros((len(seeds), resets, G, G), np.uint8)
+    rover = np.zeros((len(seeds), resets, 2), np.int32)
+    porder = np.zeros((len(seeds), resets, P, 2), np.int32)
+    tail = np.zeros((len(seeds),), np.int64)
+    obs0 = []
+    import contextlib
+    import io
+    for si, s in enumerate(seeds):
+        random.seed(s)
+        for k in range(resets):
+            with contextlib.redirect_stdout(io.StringIO()):  # the fallback prints a warning
+                o, _ = env.reset()
+            cells[si, k] = cells_of(env)
+            rover[si, k] = env.rover_pos
+            porder[si, k] = np.array(list(env.plants.keys()), np.int32).reshape(P, 2)
+            if k == 0:
+                obs0.append(o)
+        tail[si] = random.getrandbits(32)
+    np.savez_compressed(
+        os.path.join(OUT, f"maze_{name}.npz"), config=np.array(cfgt, np.int32),
+        seeds=np.array(seeds, np.int64), cells=cells, rover=rover, plant_order=porder,
+        next_u32=tail, obs0=np.array(obs0, np.float32))
+    free = (cells != OBST).reshape(len(seeds) * resets, -1).sum(1)
+    print(f"maze_{name}:", cells.shape, "free cells min/max", free.min(), free.max())
+
+
+def main_maze():
+    os.makedirs(OUT, exist_ok=True)
+    gen_maze_maps("g20", (20, 10, 12, 6, 16), [0, 1, 2, 3, 7, 42], 5)
+    gen_maze_maps("g25", (25, 10, 12, 6, 16), [0, 5, 11], 4)
+    gen_maze_maps("g13", (13, 5, 6, 3, 12), [0, 1, 2], 5)
+    gen_maze_maps("g7", (7, 3, 3, 3, 12), [0, 1, 2, 3], 6)
+    gen_maze_maps("g32", (32, 20, 30, 9, 24), [4, 9], 3)
+    gen_maze_maps("g64", (64, 100, 120, 6, 64), [0, 9], 2)
+    gen_maze_maps("g7fallback", (7, 30, 3, 3, 12), [0, 1, 2], 4)
+    gen_maze_maps("g19", (19, 120, 12, 6, 16), [3, 4], 3)
+
+
 def main_mcts():
     os.makedirs(OUT, exist_ok=True)
     gen_mcts("g7", "g7", 30, 40, 4, 40, 500, inject_cases=30)
@@ -602,5 +648,7 @@ def main_mcts():
 if __name__ == "__main__":
     if sys.argv[1:] == ["mcts"]:
         main_mcts()
+    elif sys.argv[1:] == ["maze"]:
+        main_maze()
     else:
         main()
