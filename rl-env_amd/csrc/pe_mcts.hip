@@ -130,6 +130,9 @@ struct NpStream {
   uint32_t cur;        // mt[p] (the current-round word at p)
   int head, cnt;       // ring read slot, draws buffered
   uint32_t saved_prev; // mt[625] before the last generation of position 0
+#ifdef PE_MCTS_PROF
+  uint64_t topups = 0;
+#endif
 
   __device__ void open(uint32_t* m, uint32_t* r) {
     mt = m;
@@ -188,7 +191,15 @@ struct NpStream {
     cnt += kTop;
   }
   __device__ void top_up_if_low() {
-    if (__any(cnt < kLow) && cnt <= kRing - kTop && (p & (kTop - 1)) == 0) top_up();
+    if (__any(cnt < kLow) && cnt <= kRing - kTop && (p & (kTop - 1)) == 0) {
+#ifdef PE_MCTS_PROF
+      const uint64_t t0 = __builtin_amdgcn_s_memtime();
+      top_up();
+      topups += __builtin_amdgcn_s_memtime() - t0;
+#else
+      top_up();
+#endif
+    }
   }
   // one draw straight from the stream (ring empty: before the first aligned block,
   // or a long rejection streak)
@@ -227,8 +238,36 @@ struct NpStream {
   }
   // np.random.random(): 53 bits from two draws
   __device__ double random() {
-    const uint32_t a = next() >> 5, b = next() >> 6;
-    return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+    // both ring reads issued before any branch (the ring is rarely short)
+    const uint32_t r0 = ring[head * 64], r1 = ring[((head + 1) & (kRing - 1)) * 64];
+    uint32_t a, b;
+    if (cnt >= 2) {
+      a = r0;
+      b = r1;
+      head = (head + 2) & (kRing - 1);
+      cnt -= 2;
+    } else {
+      a = next();
+      b = next();
+    }
+    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) / 9007199254740992.0;
+  }
+  // np.random.random() < 0.7, decided on the 53-bit integer: random() = N / 2^53 exactly
+  // and the double 0.7 is 6305039478318694 / 2^53, so the comparison is N < that.
+  __device__ bool random_lt_07() {
+    const uint32_t r0 = ring[head * 64], r1 = ring[((head + 1) & (kRing - 1)) * 64];
+    uint32_t a, b;
+    if (cnt >= 2) {
+      a = r0;
+      b = r1;
+      head = (head + 2) & (kRing - 1);
+      cnt -= 2;
+    } else {
+      a = next();
+      b = next();
+    }
+    const uint64_t nbits = ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
+    return nbits < 6305039478318694ull;
   }
   // np.random.randint(n): masked rejection on 32-bit draws, no draw for n == 1
   __device__ int randint(int n) {
@@ -285,8 +324,10 @@ struct GCells {
     c = s.x * G + s.y;
     nb.expl = 0;
 #pragma unroll
-    for (int q = 0; q < 5; ++q) {
-      w[q] = nbr_on_map(s, G, q) ? cw[nbr_cell(c, G, q)] : kOffMap;
+    for (int q = 0; q < 5; ++q) {  // all five loads issued together (off-map: read own cell, replace)
+      const bool on = nbr_on_map(s, G, q);
+      const uint32_t r = cw[on ? nbr_cell(c, G, q) : c];
+      w[q] = on ? r : kOffMap;
       nb.code[q] = (w[q] & kCodeMask) >> kCodeShift;
       nb.vis[q] = w[q] & kVisMask;
       nb.expl |= (w[q] & kExpl) ? 1u << q : 0u;
@@ -342,13 +383,24 @@ struct LCells {
   __device__ void load(const Sim& s, Nbr& nb) {
     c = s.x * G + s.y;
     nb.expl = 0;
+    uint32_t sat = 0;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {  // all five LDS reads issued together (off-map: read own cell, replace)
+      const bool on = nbr_on_map(s, G, q);
+      const uint32_t r = cb[on ? nbr_cell(c, G, q) : c];
+      b[q] = on ? r : ((uint32_t)OBST << kLCodeShift);
+    }
 #pragma unroll
     for (int q = 0; q < 5; ++q) {
-      b[q] = nbr_on_map(s, G, q) ? (uint32_t)cb[nbr_cell(c, G, q)] : ((uint32_t)OBST << kLCodeShift);
       nb.code[q] = b[q] >> kLCodeShift;
-      const uint32_t f = b[q] & kLSat;
-      nb.vis[q] = f < kLSat ? f : exact(nbr_cell(c, G, q));
+      nb.vis[q] = b[q] & kLSat;
+      sat |= nb.vis[q] == kLSat ? 1u << q : 0u;
       nb.expl |= (b[q] & kLExpl) ? 1u << q : 0u;
+    }
+    if (sat) {  // rare: counts of 31 or more come from global memory
+#pragma unroll
+      for (int q = 0; q < 5; ++q)
+        if (sat & (1u << q)) nb.vis[q] = exact(nbr_cell(c, G, q));
     }
   }
   __device__ void move(int q, bool set_old) {
@@ -496,6 +548,30 @@ __device__ __forceinline__ int kid_at(const MNode& nd, int j) {
 // run the same sim step together, whatever phase each is in.
 enum : int { PH_SELECT = 0, PH_EXPAND = 1, PH_ROLLOUT = 2, PH_DONE = 3 };
 
+#ifdef PE_MCTS_PROF  // diagnostics build: shader-clock cycles per phase, summed per lane
+__device__ unsigned long long g_mcts_prof[1 << 20][4];
+#define PE_MP_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define PE_MP_ACC(a_, b_, c_, d_) \
+  do {                            \
+    pa += b_ - a_;                \
+    pb += c_ - b_;                \
+    pc += d_ - c_;                \
+  } while (0)
+#define PE_MP_STORE(e_)                                                     \
+  do {                                                                      \
+    if ((e_) < (1 << 20)) {                                                 \
+      g_mcts_prof[e_][0] = pa;                                              \
+      g_mcts_prof[e_][1] = pb;                                              \
+      g_mcts_prof[e_][2] = pc;                                              \
+      g_mcts_prof[e_][3] = rng.topups;                                      \
+    }                                                                       \
+  } while (0)
+#else
+#define PE_MP_T(v)
+#define PE_MP_ACC(a_, b_, c_, d_)
+#define PE_MP_STORE(e_)
+#endif
+
 template <class CS>
 __device__ void search_env(const MctsArgs& a, int64_t e, CS& cs, uint32_t* ring) {
 #pragma clang fp contract(off)
@@ -513,6 +589,9 @@ __device__ void search_env(const MctsArgs& a, int64_t e, CS& cs, uint32_t* ring)
 
   store_node(T, 0, fresh_node(0xFFFF, 0xFF));
   int nn = 1;
+#ifdef PE_MCTS_PROF
+  uint64_t pa = 0, pb = 0, pc = 0;
+#endif
   for (int sim = 0; sim < a.n_sims; ++sim) {
     s.x = s0.x;
     s.y = s0.y;
@@ -521,35 +600,57 @@ __device__ void search_env(const MctsArgs& a, int64_t e, CS& cs, uint32_t* ring)
     s.cur_expl = root_expl;
     s.bonus = false;  // a fresh PlantOSEnv: completion_bonus_given False (:221-243)
     int node = 0, depth = 0, phase = PH_SELECT;
+    uint64_t pth0 = 0, pth1 = 0;  // node indices on the path (16 bits each), root first
+    int plen = 1;
+#define PUSH_PATH(idx)                                                 \
+  do {                                                                 \
+    if (plen < 4) pth0 |= (uint64_t)(idx) << (16 * plen);              \
+    else if (plen < 8) pth1 |= (uint64_t)(idx) << (16 * (plen - 4));   \
+    ++plen;                                                            \
+  } while (0)
     double tot = 0.0;
     MNode nd = load_node(T, 0);
-    while (phase != PH_DONE) {
+    PE_MP_T(t0);
+    // 1.-2. tree descent and expansion: a few steps, one shared sim step
+    while (phase != PH_ROLLOUT) {
       rng.top_up_if_low();
       int act = -1;
       if (phase == PH_SELECT) {
         // 1. selection (:106-114): descend while fully expanded
         if ((nd.untried & 7u) == 0u && nd.nkid > 0 && depth < a.max_depth) {
+          // a fully expanded node has all 5 children: their records load together
           const double lv = a.logt[nd.visits];
-          int best = -1;
+          MNode ch[5];
+#pragma unroll
+          for (int j = 0; j < 5; ++j) ch[j] = load_node(T, nd.kid[j]);
+          int bj = 0;
           double bw = 0.0;
-          for (int j = 0; j < nd.nkid; ++j) {
-            const int ci = kid_at(nd, j);
-            const MNode ch = load_node(T, ci);
+#pragma unroll
+          for (int j = 0; j < 5; ++j) {
             double wgt;
-            if (ch.visits == 0) {
+            if (ch[j].visits == 0) {
               wgt = INFINITY;
             } else {
-              const double exploitation = ch.value / (double)ch.visits;             // :55
-              const double exploration = a.c * sqrt(lv / (double)ch.visits);      // :56
+              const double exploitation = ch[j].value / (double)ch[j].visits;       // :55
+              const double exploration = a.c * sqrt(lv / (double)ch[j].visits);    // :56
               wgt = exploitation + exploration;                                     // :57
             }
-            if (best < 0 || wgt > bw) {  // max(): the first maximal child (:60)
-              best = ci;
+            if (j == 0 || wgt > bw) {  // max(): the first maximal child (:60)
+              bj = j;
               bw = wgt;
             }
           }
-          node = best;
-          nd = load_node(T, node);
+          int bidx = nd.kid[0];
+          MNode bn = ch[0];
+#pragma unroll
+          for (int j = 1; j < 5; ++j)
+            if (bj == j) {
+              bidx = nd.kid[j];
+              bn = ch[j];
+            }
+          node = bidx;
+          nd = bn;
+          PUSH_PATH(node);
           act = nd.action;
         } else {
           phase = PH_EXPAND;
@@ -572,58 +673,80 @@ __device__ void search_env(const MctsArgs& a, int64_t e, CS& cs, uint32_t* ring)
           store_node(T, node, nd);
           store_node(T, ci, fresh_node(node, act));
           node = ci;
+          PUSH_PATH(node);
         } else {
           phase = PH_ROLLOUT;
         }
       }
-      cs.load(s, nb);
-      if (phase == PH_ROLLOUT) {
-        // 3. rollout (:141-168), depth counts on from the descent
-        if (depth >= a.max_depth) {
-          phase = PH_DONE;
-        } else if (rng.random() < 0.7) {                          // :180
-          // _exploration_heuristic (:187-219): first strictly least-visited valid move
-          int best = -1;
-          uint32_t minv = 0;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            if (nb.code[q] != (uint32_t)OBST && (best < 0 || nb.vis[q] < minv)) {
-              best = q;
-              minv = nb.vis[q];
-            }
-          }
-          act = best >= 0 ? best : rng.randint(5);
-        } else {
-          act = rng.randint(5);                                   // :183
-        }
-      }
-      if (phase == PH_DONE) break;
+      if (phase == PH_ROLLOUT) break;
       bool te, tr;
-      const double r = sim_step(a.rl, cs, s, total, act, nb, te, tr);
+      cs.load(s, nb);
+      sim_step(a.rl, cs, s, total, act, nb, te, tr);
       if (phase == PH_SELECT) {
         depth += 1;
         if (te || tr) phase = PH_EXPAND;
-      } else if (phase == PH_EXPAND) {
-        phase = PH_ROLLOUT;
       } else {
-        tot += r;
-        depth += 1;
-        if (te || tr) {
-          if (s.expl >= total) tot += 500.0;  // exploration_percentage >= 100 (:160-163)
-          phase = PH_DONE;
-        }
+        phase = PH_ROLLOUT;
       }
     }
-    // 4. backpropagation (:130-134)
-    for (int i = node; i != 0xFFFF;) {
-      MNode b = load_node(T, i);
-      b.visits += 1;
-      b.value += tot;
-      store_node(T, i, b);
-      i = b.parent;
+    PE_MP_T(t1);
+    // 3. rollout (:141-168), depth counts on from the descent
+    for (int d = depth; d < a.max_depth; ++d) {
+      rng.top_up_if_low();
+      cs.load(s, nb);
+      int act;
+      if (rng.random_lt_07()) {                                   // np.random.random() < 0.7 (:180)
+        // _exploration_heuristic (:187-219): first strictly least-visited valid move
+        int best = -1;
+        uint32_t minv = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (nb.code[q] != (uint32_t)OBST && (best < 0 || nb.vis[q] < minv)) {
+            best = q;
+            minv = nb.vis[q];
+          }
+        }
+        act = best >= 0 ? best : rng.randint(5);
+      } else {
+        act = rng.randint(5);                                     // :183
+      }
+      bool te, tr;
+      const double r = sim_step(a.rl, cs, s, total, act, nb, te, tr);
+      tot += r;
+      if (te || tr) {
+        if (s.expl >= total) tot += 500.0;  // exploration_percentage >= 100 (:160-163)
+        break;
+      }
+    }
+    PE_MP_T(t2);
+    // 4. backpropagation (:130-134): the path's records load together when it is
+    // short (the usual case), else walk the parent links
+    if (plen <= 8) {
+      MNode pb[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k < plen) pb[k] = load_node(T, (int)(((k < 4 ? pth0 : pth1) >> (16 * (k & 3))) & 0xFFFFu));
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k < plen) {
+          pb[k].visits += 1;
+          pb[k].value += tot;
+          store_node(T, (int)(((k < 4 ? pth0 : pth1) >> (16 * (k & 3))) & 0xFFFFu), pb[k]);
+        }
+    } else {
+      for (int i = node; i != 0xFFFF;) {
+        MNode b = load_node(T, i);
+        b.visits += 1;
+        b.value += tot;
+        store_node(T, i, b);
+        i = b.parent;
+      }
     }
     cs.undo();  // the next simulation starts from a fresh copy (:104)
+    PE_MP_T(t3);
+    PE_MP_ACC(t0, t1, t2, t3);
   }
+  PE_MP_STORE(e);
   // best_action (:62-69)
   const MNode root = load_node(T, 0);
   int act;
@@ -983,5 +1106,13 @@ int pe_mcts_search(pe_mcts* m, const uint8_t* mask, int32_t* actions, int32_t* r
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? PE_OK : hip_fail(e, "pe_mcts_search");
 }
+
+#ifdef PE_MCTS_PROF
+int pe_mcts_debug_prof(uint64_t* host, int64_t count) {
+  if (count > (int64_t)(1 << 20) * 4) count = (int64_t)(1 << 20) * 4;
+  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mcts_prof), (size_t)count * 8);
+  return e == hipSuccess ? PE_OK : hip_fail(e, "hipMemcpyFromSymbol");
+}
+#endif
 
 }  // extern "C"
