@@ -178,3 +178,26 @@ def test_masked_search_leaves_other_envs():
     assert (pos1[~off] != pos0[~off]).any()
     m.close()
     b.close()
+
+
+def test_mcts_drives_the_vec_env():
+    """INTEGRATION.md's loop: MCTS over a PlantOSVecEnv, actions stepped on the device."""
+    from plantos_amd import PlantOSVecEnv
+    from plantos_amd.mcts import MCTS
+    env = PlantOSVecEnv(16, grid_size=25, num_plants=10, num_obstacles=12, lidar_range=6, lidar_channels=16,
+                        tensors=True, device="cuda:0", seed=4)
+    mcts = MCTS(env, n_simulations=12, c_param=1.414, max_depth=20, seed=0)
+    cfg = O.config(25, 10, 12, 6, 16)
+    streams = {e: O.NpMT(e) for e in (0, 7, 15)}  # env e: np.random.seed(0 + e), continuing across decisions
+    obs = env.reset()
+    for _ in range(5):
+        st = env.batch.get_state()
+        actions = mcts.search(obs)
+        torch.cuda.synchronize()
+        a = np_(actions).copy()
+        cells, visits, expl, sc = (np_(st[k]) for k in ("cells", "visits", "explored", "scalars"))
+        for e, r in streams.items():
+            assert O.mcts_search(cfg, cells[e], visits[e], expl[e], sc[e], r, 12, 1.414, 20)[0] == a[e]
+        obs, rew, dones, infos = env.step(actions)
+        assert ((a >= 0) & (a <= 4)).all()
+    env.close()
