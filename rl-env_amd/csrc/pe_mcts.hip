@@ -874,6 +874,7 @@ struct DevBind {
   int prev = -1;
   hipError_t err = hipSuccess;
   explicit DevBind(int dev) {
+    (void)hipGetLastError();  // drop a stale error of an earlier call (launch checks below)
     int cur = -1;
     err = hipGetDevice(&cur);
     if (err == hipSuccess && cur != dev) {

@@ -1134,6 +1134,10 @@ struct DeviceGuard {
   int prev = -1;
   int rc = PE_OK;
   explicit DeviceGuard(const pe_handle* h) {
+    // hipGetLastError() reports the last failed runtime call of this thread,
+    // whoever made it (torch probes, the caller's own calls): drop such a stale
+    // error so the launch checks below see only this call's launches.
+    (void)hipGetLastError();
     hipError_t e = hipGetDevice(&prev);
     if (e != hipSuccess) {
       rc = hip_fail(e, "hipGetDevice");
@@ -1298,6 +1302,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   hipError_t he = hipGetDeviceCount(&ndev);
   if (he != hipSuccess || ndev == 0) return fail(PE_ERR_DEVICE, "no HIP device available (no CPU fallback)");
   if (device < 0 || device >= ndev) return fail(PE_ERR_ARG, "bad device index");
+  (void)hipGetLastError();  // stale error of an earlier call (see DeviceGuard)
   struct Restore {
     int prev = -1;
     ~Restore() {

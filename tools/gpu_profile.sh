@@ -17,7 +17,7 @@ BENCH_ARGS="--steps 2000 --warmup 200 --no-cpu-baseline"
 for w in $WHAT; do
   case $w in
     tests)
-      timeout -k 10 900 python -m pytest tests -m gpu -x -q > $OUT/tests_$TAG.log 2>&1 ;;
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/tests_$TAG.log 2>&1 ;;
     bench)
       timeout -k 10 300 python bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err ;;
     bench64)
