@@ -39,8 +39,9 @@ def algorithmic_bytes(C, R):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=2000)
-    p.add_argument("--warmup", type=int, default=200)
+    # >= 1e10 env-steps timed after a 1000-step warm-up (153000 x 65536 envs ~ 1.7 s)
+    p.add_argument("--steps", type=int, default=153000)
+    p.add_argument("--warmup", type=int, default=1000)
     p.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     p.add_argument("--grid", type=int, default=20)
     p.add_argument("--plants", type=int, default=None)
@@ -73,7 +74,17 @@ def cpu_baseline(args, plants, obstacles):
     secs, _ = O.bench(cfg, n_envs, steps, args.seed, threads)
     return {"value": n_envs * steps / secs, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": f"{n_envs} envs x {steps} steps ({secs:.1f} s) of the same synthetic workload, "
-                      f"oracle/plantos_oracle.c, OpenMP {threads} threads"}
+                      f"oracle/plantos_oracle.c, OpenMP {threads} threads on {cpu_model()}"}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
 
 
 def measured_traffic(cfg):

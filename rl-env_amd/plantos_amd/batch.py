@@ -53,9 +53,12 @@ class PlantOSBatch:
         self._h = h
         n, D, dev = self.num_envs, self.obs_dim, self.device
         self.obs = torch.zeros((n, D), dtype=torch.float32, device=dev)
-        self.reward = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.terminated = torch.zeros(n, dtype=torch.uint8, device=dev)
-        self.truncated = torch.zeros(n, dtype=torch.uint8, device=dev)
+        # reward f32 | terminated u8 | truncated u8 in ONE device buffer: a host-side
+        # consumer fetches the per-step scalars with a single device->host copy
+        self._packed = torch.zeros(6 * n, dtype=torch.uint8, device=dev)
+        self.reward = self._packed[:4 * n].view(torch.float32)
+        self.terminated = self._packed[4 * n:5 * n]
+        self.truncated = self._packed[5 * n:]
         self.terminal_obs = torch.zeros((n, D), dtype=torch.float32, device=dev)
         self.episode_return = torch.zeros(n, dtype=torch.float64, device=dev)
         self.episode_length = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -87,6 +90,12 @@ class PlantOSBatch:
         if not self._h:
             raise ValueError("PlantOSBatch is closed")
         return self._h
+
+    @property
+    def packed_outputs(self):
+        """u8 [6n] device view of one step's scalars: reward (f32 [n]) |
+        terminated (u8 [n]) | truncated (u8 [n])."""
+        return self._packed
 
     @property
     def kernel_name(self):

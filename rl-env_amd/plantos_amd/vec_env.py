@@ -135,21 +135,50 @@ class LazyInfos(list):
 
 
 class _StepView:
-    """Host views of one step's device outputs, copied lazily (once each)."""
+    """Host views of one step's device outputs, copied lazily (once each).
 
-    def __init__(self, venv, done_np, term_np, trunc_np):
+    The done/terminated/truncated flags are either host arrays already or a
+    device u8 [2n] (terminated | truncated) copy fetched on first access (the
+    zero-copy face: a loop that never reads infos never synchronizes)."""
+
+    def __init__(self, venv, done_np=None, term_np=None, trunc_np=None, dev_flags=None):
         self.v = venv
-        self.done = done_np
-        self.term = term_np
-        self.trunc = trunc_np
+        self._flags = None if dev_flags is not None else (done_np, term_np, trunc_np)
+        self._dev_flags = dev_flags
         self._info = None
         self._tinfo = None
         self._tobs = None
         self._ret = None
         self._len = None
-        self._done_idx = np.nonzero(done_np)[0]
+        self._didx = None
         self._t = round(time.time() - venv._t_start, 6)
         self._expired = False
+
+    def _host_flags(self):
+        if self._flags is None:
+            f = self._dev_flags.cpu().numpy().astype(bool)  # own copy: valid after expiry
+            n = f.shape[0] // 2
+            te, tr = f[:n], f[n:]
+            self._flags = (te | tr, te, tr)
+        return self._flags
+
+    @property
+    def done(self):
+        return self._host_flags()[0]
+
+    @property
+    def term(self):
+        return self._host_flags()[1]
+
+    @property
+    def trunc(self):
+        return self._host_flags()[2]
+
+    @property
+    def _done_idx(self):
+        if self._didx is None:
+            self._didx = np.nonzero(self.done)[0]
+        return self._didx
 
     def expire(self):
         """The next step overwrites the device buffers this view reads lazily."""
@@ -201,7 +230,7 @@ class PlantOSVecEnv(_VecEnvBase):
     def __init__(self, num_envs, grid_size=21, num_plants=8, num_obstacles=50, lidar_range=2, lidar_channels=10,
                  thirsty_plant_prob=0.7, max_steps=1000, seed=0, device=None, tensors=False, env_id_offset=0,
                  observation_mode="lidar", render_mode=None, batch=None, reset_mode="device", python_seed=None,
-                 curriculum=False, map_generation_algo="original"):
+                 curriculum=False, map_generation_algo="original", host_buffers=0):
         """reset_mode="device": maps from the device generator keyed by (seed, env id,
         episode) -- the throughput mode.  reset_mode="cpython": the reference's own
         layouts, seed-exact: CPython's global `random` after random.seed(python_seed)
@@ -210,7 +239,11 @@ class PlantOSVecEnv(_VecEnvBase):
         CurriculumWrapper of A2C_training.py:37-109 to every env, as
         make_env_wrapper(use_curriculum=True) does (A2C_training.py:114-126).
         map_generation_algo="maze" selects the fork's maze layouts
-        (gradio-app/plantos_env_new.py:28, 408-604) in either reset mode."""
+        (gradio-app/plantos_env_new.py:28, 408-604) in either reset mode.
+        host_buffers=k (numpy face): obs arrive in a ring of k pinned host buffers
+        (one DMA at full PCIe rate; each returned obs array stays valid for k steps,
+        enough for SB3's collect_rollouts with k >= 2); 0 (default): a fresh array
+        per step, as DummyVecEnv returns."""
         if observation_mode != "lidar":
             raise ValueError("only observation_mode='lidar' exists in the reference (plantos_env.py:27)")
         if reset_mode not in ("device", "cpython"):
@@ -237,6 +270,10 @@ class PlantOSVecEnv(_VecEnvBase):
         self.thirsty_plant_prob, self.max_steps = thirsty_plant_prob, max_steps
         self.render_mode = render_mode
         self.tensors = bool(tensors)
+        self.host_buffers = int(host_buffers)
+        self._pinned_packed = None
+        self._pinned_obs = None
+        self._ring = 0
         obs_space, act_space = make_spaces(self.batch.obs_dim)
         if _VecEnvBase is not object:  # pragma: no cover
             super().__init__(num_envs, obs_space, act_space)
@@ -259,11 +296,44 @@ class PlantOSVecEnv(_VecEnvBase):
         fresh = self.batch.load_maps(idx, cells, rover)
         self.batch.obs[torch.as_tensor(idx, device=self.batch.device)] = fresh
 
-    def _new_view(self, done_np, te_np, tr_np):
+    def _new_view(self, done_np=None, te_np=None, tr_np=None, dev_flags=None):
         if self._last_view is not None:
             self._last_view.expire()
-        self._last_view = _StepView(self, done_np, te_np, tr_np)
+        self._last_view = _StepView(self, done_np, te_np, tr_np, dev_flags=dev_flags)
         return self._last_view
+
+    def _to_host(self, obs):
+        """(obs, reward, terminated, truncated) as numpy with ONE stream sync: the
+        packed per-step scalars go to a pinned buffer asynchronously, the obs
+        either into the pinned ring (host_buffers > 0: views valid for that many
+        steps) or into a fresh array (obs.cpu(), which synchronizes the stream
+        after both copies)."""
+        b = self.batch
+        packed = getattr(b, "packed_outputs", None)
+        if packed is None or not packed.is_cuda:  # e.g. the oracle-backed batch of the CPU tests
+            return (obs.cpu().numpy(), b.reward.cpu().numpy(), b.terminated.cpu().numpy().astype(bool),
+                    b.truncated.cpu().numpy().astype(bool))
+        n = self.num_envs
+        if self._pinned_packed is None:
+            self._pinned_packed = torch.empty(packed.shape, dtype=torch.uint8, pin_memory=True)
+        hp = self._pinned_packed
+        hp.copy_(packed, non_blocking=True)
+        if self.host_buffers:
+            if self._pinned_obs is None:
+                self._pinned_obs = [torch.empty(obs.shape, dtype=obs.dtype, pin_memory=True)
+                                    for _ in range(self.host_buffers)]
+            ho = self._pinned_obs[self._ring]
+            self._ring = (self._ring + 1) % self.host_buffers
+            ho.copy_(obs, non_blocking=True)
+            torch.cuda.current_stream(b.device).synchronize()
+            obs_np = ho.numpy()
+        else:
+            obs_np = obs.cpu().numpy()
+        hn = hp.numpy()
+        rew = hn[:4 * n].view(np.float32).copy()
+        te = hn[4 * n:5 * n].astype(bool)
+        tr = hn[5 * n:].astype(bool)
+        return obs_np, rew, te, tr
 
     def reset(self):
         """All envs get a fresh map; returns obs [N, D]."""
@@ -291,20 +361,20 @@ class PlantOSVecEnv(_VecEnvBase):
             a = torch.as_tensor(np.asarray(a).reshape(-1).astype(np.int64), device=self.batch.device)
         obs, rew, te, tr = self.batch.step(a.reshape(-1))
         self._actions = None
-        done = te.bool() | tr.bool()
         if self.reset_mode == "cpython":  # DummyVecEnv: done envs reset in index order
-            idx = torch.nonzero(done).reshape(-1).cpu().numpy()
+            idx = torch.nonzero(te.bool() | tr.bool()).reshape(-1).cpu().numpy()
             if len(idx):
                 self._load_stream_maps(idx)
         if self.tensors:
-            done_np, te_np, tr_np = (x.cpu().numpy() for x in (done, te.bool(), tr.bool()))
-            out = (obs.clone(), rew.clone(), done)
-        else:
-            obs_np, rew_np = obs.cpu().numpy(), rew.cpu().numpy()
-            done_np, te_np, tr_np = done.cpu().numpy(), te.cpu().numpy().astype(bool), tr.cpu().numpy().astype(bool)
-            out = (obs_np, rew_np, done_np)
+            n = self.num_envs
+            packed = getattr(self.batch, "packed_outputs", None)
+            flags = packed[4 * n:].clone() if packed is not None else torch.cat([te, tr]).to(torch.uint8)
+            infos = LazyInfos(n, self._new_view(dev_flags=flags))
+            return obs.clone(), rew.clone(), (te | tr).bool(), infos
+        obs_np, rew_np, te_np, tr_np = self._to_host(obs)
+        done_np = te_np | tr_np
         infos = LazyInfos(self.num_envs, self._new_view(done_np, te_np, tr_np))
-        return out[0], out[1], out[2], infos
+        return obs_np, rew_np, done_np, infos
 
     def step(self, actions):
         self.step_async(actions)

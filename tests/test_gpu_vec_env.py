@@ -44,6 +44,42 @@ def test_vec_env_gpu_vs_oracle(cfg, n, T, max_steps):
     gpu.close()
 
 
+def test_host_faces_agree():
+    """The numpy face with a pinned obs ring (host_buffers=3) and the zero-copy
+    face (tensors=True, flags fetched lazily) return what the default numpy face
+    returns, step for step, across auto-resets; ring arrays stay valid for 3 steps."""
+    cfg = dict(grid_size=20, num_plants=10, num_obstacles=12, lidar_range=6, lidar_channels=16)
+    n, seed, ms = 200, 5, 40
+    envs = [PlantOSVecEnv(n, seed=seed, max_steps=ms, device="cuda:0", **cfg),
+            PlantOSVecEnv(n, seed=seed, max_steps=ms, device="cuda:0", host_buffers=3, **cfg),
+            PlantOSVecEnv(n, seed=seed, max_steps=ms, device="cuda:0", tensors=True, **cfg)]
+    for v in envs:
+        v.reset()
+    rng = np.random.default_rng(8)
+    kept = []
+    for t in range(90):
+        a = rng.integers(0, 5, n)
+        out = [v.step(a if i < 2 else torch.as_tensor(a, device="cuda:0")) for i, v in enumerate(envs)]
+        (o0, r0, d0, i0), (o1, r1, d1, i1), (o2, r2, d2, i2) = out
+        o2, r2, d2 = o2.cpu().numpy(), r2.cpu().numpy(), d2.cpu().numpy()
+        assert (o0 == o1).all() and (o0 == o2).all() and (r0 == r1).all() and (r0 == r2).all(), t
+        assert (d0 == d1).all() and (d0 == d2).all() and r1.dtype == np.float32 and d1.dtype == bool
+        for e in list(np.nonzero(d0)[0][:3]) + [1]:
+            a0, a1, a2 = i0[e], i1[e], i2[e]
+            assert a0.keys() == a1.keys() == a2.keys()
+            if "terminal_observation" in a0:
+                assert (a0["terminal_observation"] == a2["terminal_observation"]).all()
+                assert a0["TimeLimit.truncated"] == a1["TimeLimit.truncated"] == a2["TimeLimit.truncated"]
+                assert a0["episode"]["r"] == a2["episode"]["r"]
+        kept.append((o1, o0.copy()))
+        if len(kept) > 3:
+            kept.pop(0)
+        for ring_view, copy in kept:  # the last 3 ring arrays are intact
+            assert (ring_view == copy).all()
+    for v in envs:
+        v.close()
+
+
 def test_vec_env_tensor_mode_and_gym_face():
     cfg = dict(grid_size=20, num_plants=10, num_obstacles=12, lidar_range=6, lidar_channels=16)
     v = PlantOSVecEnv(64, tensors=True, device="cuda:0", **cfg)

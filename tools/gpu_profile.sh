@@ -20,6 +20,8 @@ for w in $WHAT; do
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/tests_$TAG.log 2>&1 ;;
     bench)
       timeout -k 10 300 python bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err ;;
+    benchq)
+      timeout -k 10 300 python bench.py --steps 4000 --warmup 200 --no-cpu-baseline > $OUT/benchq_$TAG.json 2> $OUT/benchq_$TAG.err ;;
     bench64)
       timeout -k 10 300 python bench.py --grid 64 --rays 64 --range 6 --steps 500 --warmup 50 \
         --cpu-seconds 5 > $OUT/bench64_$TAG.json 2> $OUT/bench64_$TAG.err ;;
@@ -36,6 +38,14 @@ for w in $WHAT; do
         python3 bench.py --grid 64 --rays 64 --steps 30 --warmup 5 --no-cpu-baseline > $OUT/pmc64_fetch_$TAG.json 2> $OUT/pmc64_fetch_$TAG.err
       timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $OUT/pmc64_write_$TAG -o run -- \
         python3 bench.py --grid 64 --rays 64 --steps 30 --warmup 5 --no-cpu-baseline > $OUT/pmc64_write_$TAG.json 2> $OUT/pmc64_write_$TAG.err ;;
+    sq)
+      timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU \
+        SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY --kernel-trace -f csv -d $OUT/sq_$TAG -o run -- \
+        python3 bench.py --steps 50 --warmup 10 --no-cpu-baseline > $OUT/sq_$TAG.json 2> $OUT/sq_$TAG.err ;;
+    sq64)
+      timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU \
+        SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY --kernel-trace -f csv -d $OUT/sq64_$TAG -o run -- \
+        python3 bench.py --grid 64 --rays 64 --steps 30 --warmup 5 --no-cpu-baseline > $OUT/sq64_$TAG.json 2> $OUT/sq64_$TAG.err ;;
     micro)
       timeout -k 10 300 python tools/micro_step.py > $OUT/micro_$TAG.json 2> $OUT/micro_$TAG.err ;;
     *) echo "unknown step $w" >&2; exit 2 ;;
