@@ -146,6 +146,20 @@ struct Scal {
   uint32_t flags, episode;
 };
 
+// Write-through (sc1) stores for the per-step state commit: a relaxed agent-scope
+// atomic store is a plain store with sc1 (MI355X: the line goes on to the
+// Infinity Cache / HBM at once instead of staying dirty in the XCD's L2), so the
+// kernel-end L2 writeback has nothing of it left to flush at the launch boundary.
+template <typename T>
+__device__ __forceinline__ void st_wt(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(uint4* p, uint4 v) {
+  uint64_t* q = reinterpret_cast<uint64_t*>(p);
+  st_wt(q, (uint64_t)v.x | ((uint64_t)v.y << 32));
+  st_wt(q + 1, (uint64_t)v.z | ((uint64_t)v.w << 32));
+}
+
 __device__ __forceinline__ Scal unpack(uint4 w) {
   Scal s;
   s.x = w.x & 0xFF;

@@ -231,7 +231,10 @@ __device__ __forceinline__ void store_tile(const float* rows, float* dst, int va
       const v4f* sv = reinterpret_cast<const v4f*>(rows);
       for (int k = threadIdx.x; k < n4; k += blockDim.x) {
         const v4f v = sv[k];
-        asm volatile("global_store_dwordx4 %0, %1, off " PE_OBS_STORE_ASM ::"v"(d4 + k), "v"(v) : "memory");
+        // s_nop 1: a 128-bit store reads its data VGPRs after issue; nothing inside
+        // the asm pads that hazard for hipcc's next write of them
+        asm volatile("global_store_dwordx4 %0, %1, off " PE_OBS_STORE_ASM "\n\ts_nop 1" ::"v"(d4 + k), "v"(v)
+                     : "memory");
       }
 #elif defined(PE_OBS_STORE_NT)
       typedef float v4f __attribute__((ext_vector_type(4)));
@@ -748,7 +751,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
       // ---- commit (plantos_env.py:160-222)
       if (ok) {
         const int pb = (4 * (ny + 2)) & 31;
-        st.vis[e * g.vstride + (int64_t)nx * g.NW + pbw] = (vraw & ~(0xFu << pb)) | (nib << pb);
+        st_wt(st.vis + e * g.vstride + (int64_t)nx * g.NW + pbw, (vraw & ~(0xFu << pb)) | (nib << pb));
         visit_bump_exact(st, g, e, cell_n, n);
         if (s.flags & F_EXPL_BITMAP) {                            // explored[old]=1, [new]=2 (:198-200)
           const uint32_t bo = 1u << (cell_o & 31), bn = 1u << (cell_n & 31);
@@ -770,9 +773,9 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
       if (watered) {
         const int bit = 2 * (s.y + R);
         if constexpr (ONEWORD) {
-          const_cast<uint64_t*>(gb)[s.x] = lrow[(R + 1) * EPB + lane] & ~(1ull << bit);  // code 3 -> 2
+          st_wt(const_cast<uint64_t*>(gb) + s.x, (uint64_t)(lrow[(R + 1) * EPB + lane] & ~(1ull << bit)));  // code 3 -> 2
         } else {
-          const_cast<uint64_t*>(gb)[(int64_t)s.x * g.WPR + (bit >> 6)] = craw & ~(1ull << (bit & 63));
+          st_wt(const_cast<uint64_t*>(gb) + (int64_t)s.x * g.WPR + (bit >> 6), (uint64_t)(craw & ~(1ull << (bit & 63))));
         }
       }
       if (bad) {
@@ -795,11 +798,11 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
       }
       if (st.cur) term = curriculum_hit(st.cur, e, cthr, s.expl, s.total) || term;  // A2C_training.py:101-103
       ret += rew;
-      a.reward[e] = (float)rew;
-      a.term[e] = term;
-      a.trunc[e] = trunc;
-      st.ep_ret[e] = ret;
-      st.scal[e] = pack(s);
+      st_wt(a.reward + e, (float)rew);
+      st_wt(a.term + e, (uint8_t)term);
+      st_wt(a.trunc + e, (uint8_t)trunc);
+      st_wt(st.ep_ret + e, ret);
+      st_wt(st.scal + e, pack(s));
       done = term || trunc;  // terminal outputs; the reset itself only with autoreset
     }
   }
