@@ -54,6 +54,9 @@ def parse():
     p.add_argument("--graph", type=int, default=64,
                    help="capture this many consecutive steps in one hipGraph and replay it (0: one host "
                         "launch per step); every captured step is a full pe_step launch")
+    p.add_argument("--desync", action="store_true",
+                   help="steady-state episode mix: env e starts at a random step count in [0, max_steps), so "
+                        "about n/1000 envs auto-reset in every step (default: synchronized fresh episodes)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     return p.parse_args()
@@ -135,6 +138,13 @@ def main():
         n_, grid_size=G, num_plants=plants, num_obstacles=obstacles, lidar_range=R, lidar_channels=C,
         device=device, **kw))
     b = shard.batch
+    if args.desync:
+        from plantos_amd import _capi as CA
+        st = b.get_state()
+        sc = st["scalars"]
+        g = torch.Generator(device="cpu").manual_seed(args.seed + 1)
+        sc[:, CA.PE_S_STEP] = torch.randint(0, 1000, (n,), generator=g, dtype=torch.int32).to(sc.device)
+        b.set_state(scalars=sc)
     T = args.action_steps
     actions = torch.empty((T, n), dtype=torch.int32, device=device)
     for t in range(T):
@@ -203,7 +213,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32/f32",
-            "data": "synthetic (device-rng maps, philox actions)",
+            "data": "synthetic (device-rng maps, philox actions" + (", desynchronized episodes)" if args.desync
+                                                                     else ")"),
             "config": {"workload": f"{n} envs/GPU, {G}x{G} grid, {C} rays, range {R}, {plants} plants, "
                                    f"{obstacles} obstacles, auto-reset, actions in HBM",
                        "envs_per_gpu": n, "grid": G, "rays": C, "lidar_range": R,

@@ -14,7 +14,7 @@ SRC = os.path.join(HERE, "csrc", "plantos_batch.hip")
 SRC_HOST = os.path.join(HERE, "csrc", "pe_pystream.cpp")
 SRC_MCTS = os.path.join(HERE, "csrc", "pe_mcts.hip")
 DEPS = [SRC, SRC_HOST, SRC_MCTS] + [os.path.join(HERE, "csrc", f) for f in
-                                    ("pe_device.hpp", "pe_fast.hpp", "pe_quad.hpp", "pe_handle.hpp")] + [
+                                    ("pe_device.hpp", "pe_fast.hpp", "pe_quad.hpp", "pe_coop.hpp", "pe_handle.hpp")] + [
     os.path.join(REPO, "include", "plantos_batch.h"), os.path.join(HERE, "tools_gen_lidar.py")]
 OUT = os.path.join(HERE, "plantos_amd", "libplantos_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

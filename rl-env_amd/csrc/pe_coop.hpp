@@ -1,0 +1,404 @@
+// pe_coop.hpp -- wave-cooperative auto-reset: one env's reset() by all 64 lanes.
+//
+// The lane-per-env reset (gen_map + build_obs_fresh in pe_device.hpp /
+// plantos_batch.hip) is a serial chain of ~60k instructions per env: scans of
+// the grid image per plant pick, rejection loops, per-lane row stores.  That is
+// fine when every lane of the commit wave has an env to reset (a synchronized
+// batch truncating together), but inside a step it is the whole block's latency:
+// a step in which ANY env of a block auto-resets took ~100 us instead of ~11 us,
+// and steady-state training (episodes ending at different steps) resets a few
+// envs in every step.
+//
+// Here the wave that owns a done env generates its map cooperatively: lane r
+// holds grid row r in registers (G <= 64), the per-row counts of candidate cells
+// are prefix-summed across lanes once, and each draw of random.sample /
+// random.choice (plantos_env.py:366-372) finds its row with one ballot and its
+// column with a ballot over the row word's set bits.  The draws are the same
+// device-rng (Philox) stream in the same order as gen_map, so the map is the one
+// gen_map / the oracle's po_reset_philox produce (the GPU parity tests check it).
+// The stream itself is generated 64 blocks at a time (lane k: block base+k) and
+// each draw is one readlane.  The terminal info, the fresh observation (lane i
+// marches ray i over rows fetched from their owner lanes) and the row stores are
+// wave-parallel too.
+//
+// MAXW: grid-row words a lane holds (1 when G + 2R <= 32, else up to kCoopWPR).
+#pragma once
+#include "../../include/plantos_batch.h"
+#include "pe_device.hpp"
+
+namespace pe {
+
+constexpr int kCoopWPR = 4;     // row words per lane: G + 2R <= 128
+constexpr int kCoopMaxDone = 8; // done envs per block up to which the cooperative path is taken
+
+// The cooperative path covers the original map generator with one grid row per
+// lane; everything else takes the lane-per-env path.
+__host__ __device__ constexpr bool coop_reset_ok(int G, int WPR, int NW, int P, int C, int map_algo) {
+  return G <= 64 && WPR <= kCoopWPR && NW <= kMaxNW && P <= 128 && C <= 64 && map_algo == 0;
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(v, o);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+  return (uint64_t)(uint32_t)__shfl((int)(uint32_t)v, src) |
+         ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), src) << 32);
+}
+
+// bit position of the jj-th (0-based) set bit of the wave-uniform mask m
+__device__ __forceinline__ int nth_set_bit(uint64_t m, int jj, int lane) {
+  const bool bit = (m >> lane) & 1ull;
+  const int rank = __popcll(m & ((1ull << lane) - 1ull));
+  const uint64_t hit = __ballot(bit && rank == jj);
+  return __ffsll((unsigned long long)hit) - 1;
+}
+
+// A lane's grid row: MAXW named words, read and written by mask-selects.  (A
+// word array indexed by a computed word number becomes a dynamically indexed
+// stack array, i.e. scratch memory for the whole kernel.)
+template <int MAXW>
+struct Row4 {
+  uint64_t w0, w1, w2, w3;
+  __device__ __forceinline__ uint64_t get(int i) const {
+    if constexpr (MAXW == 1) {
+      return w0;
+    } else {
+      const uint64_t m0 = 0ull - (uint64_t)(i == 0), m1 = 0ull - (uint64_t)(i == 1);
+      const uint64_t m2 = 0ull - (uint64_t)(i == 2), m3 = 0ull - (uint64_t)(i == 3);
+      return (w0 & m0) | (w1 & m1) | (w2 & m2) | (w3 & m3);
+    }
+  }
+  __device__ __forceinline__ void set(int i, uint64_t v) {
+    if constexpr (MAXW == 1) {
+      w0 = v;
+    } else {
+      w0 = i == 0 ? v : w0;
+      w1 = i == 1 ? v : w1;
+      w2 = i == 2 ? v : w2;
+      w3 = i == 3 ? v : w3;
+    }
+  }
+};
+
+// The device-rng reset stream (pe_device.hpp Stream: Philox4x32-10 blocks 0, 1,
+// 2, ... keyed by (seed, env, episode), words x, y, z, w in order) for a whole
+// wave: lane k computes block base+k (one VALU Philox pass = 256 words; a map
+// takes ~50), transposed once so that word 64j+k sits in register cj of lane k;
+// a draw is then one uniform register select and one readlane -- no branches,
+// no serial scalar multiply chain.  (The selects are mask arithmetic: a
+// divergent branch around them would make the cursor look divergent.)
+struct WaveStream {
+  uint32_t k0, k1, env, episode, base;
+  uint32_t c0, c1, c2, c3;  // lane k: words k, 64+k, 128+k, 192+k of blocks base..base+63
+  int pos;                  // next word (uniform)
+  __device__ __forceinline__ static uint32_t pick4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, int i) {
+    const uint32_t m0 = 0u - (uint32_t)(i == 0), m1 = 0u - (uint32_t)(i == 1);
+    const uint32_t m2 = 0u - (uint32_t)(i == 2), m3 = 0u - (uint32_t)(i == 3);
+    return (a & m0) | (b & m1) | (c & m2) | (d & m3);
+  }
+  __device__ __forceinline__ void fill(int lane) {
+    const uint4 b = philox(make_uint4(base + (uint32_t)lane, env, episode, kDomainReset), k0, k1);
+    uint32_t t[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // word 64j + lane = component lane&3 of block 16j + lane/4
+      const int src = 16 * j + (lane >> 2);
+      t[j] = pick4((uint32_t)__shfl((int)b.x, src), (uint32_t)__shfl((int)b.y, src),
+                   (uint32_t)__shfl((int)b.z, src), (uint32_t)__shfl((int)b.w, src), lane & 3);
+    }
+    c0 = t[0];
+    c1 = t[1];
+    c2 = t[2];
+    c3 = t[3];
+    pos = 0;
+  }
+  __device__ __forceinline__ void init(uint64_t seed, uint32_t env_id, uint32_t ep, int lane) {
+    k0 = (uint32_t)seed;
+    k1 = (uint32_t)(seed >> 32);
+    env = env_id;
+    episode = ep;
+    base = 0;
+    fill(lane);
+  }
+  __device__ __forceinline__ uint32_t next(int lane) {
+    if (pos == 256) {  // rare: a map takes ~50 words
+      base += 64;
+      fill(lane);
+    }
+    const int p = pos++;
+    return (uint32_t)__builtin_amdgcn_readlane((int)pick4(c0, c1, c2, c3, p >> 6), p & 63);
+  }
+  // random.py:239-248 _randbelow_with_getrandbits (getrandbits(k) = u32 >> (32-k))
+  __device__ __forceinline__ uint32_t below(uint32_t n, int lane) {
+    if (!n) return 0;
+    const int k = 32 - __clz(n);
+    uint32_t r = next(lane) >> (32 - k);
+    while (r >= n) r = next(lane) >> (32 - k);
+    return r;
+  }
+  // random.random()
+  __device__ __forceinline__ double random53(int lane) {
+    const uint32_t a = next(lane) >> 5, b = next(lane) >> 6;
+    return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
+  }
+};
+
+// code `code` at padded column pcol of this lane's row words
+template <int MAXW>
+__device__ __forceinline__ void coop_set(Row4<MAXW>& rw, int pcol, int code) {
+  const int bit = 2 * pcol;
+  const uint64_t v = rw.get(bit >> 6);
+  rw.set(bit >> 6, (v & ~(3ull << (bit & 63))) | ((uint64_t)code << (bit & 63)));
+}
+
+// Candidate-cell mask of one row word: kind 0 = not an obstacle (random.sample's
+// `available`, :358-366), kind 1 = empty (the rover's `available - plants`, :370-372)
+__device__ __forceinline__ uint64_t cand_mask(uint64_t v, uint64_t real, int kind) {
+  const uint64_t lo = v & kEven64, hi = (v >> 1) & kEven64;
+  return kind == 0 ? (real & ~(lo & ~hi)) : (real & ~(lo | hi));
+}
+
+// The j-th candidate cell (row-major) given this lane's inclusive/exclusive
+// prefix counts; returns the row and the padded column (both uniform).
+template <int MAXW>
+__device__ __forceinline__ void coop_nth_cell(const Row4<MAXW>& rw, int WPR, const uint64_t* real, int incl,
+                                              int excl, int j, int kind, int lane, int& row, int& pcol) {
+  row = __popcll(__ballot(incl <= j));  // rows before it hold <= j candidates
+  int jj = j - __builtin_amdgcn_readlane(excl, row);
+  pcol = 0;
+#pragma unroll
+  for (int w = 0; w < MAXW; ++w) {
+    if (MAXW == 1 || w < WPR) {
+      const uint64_t m = cand_mask(readlane64(rw.get(w), row), real[w], kind);
+      const int c = __popcll(m);
+      if (MAXW == 1 || (jj >= 0 && jj < c)) pcol = w * 32 + nth_set_bit(m, jj, lane) / 2;
+      jj -= c;
+    }
+  }
+}
+
+// gen_map (pe_device.hpp, original algorithm) for one env by one wave: the same
+// Philox draws in the same order, rows in the lanes' registers.  Returns the new
+// scalars (uniform); rw holds the lane's grid row.  tab: the handle's tables in
+// global memory (uniform words: scalar loads).
+template <int MAXW>
+__device__ inline Scal coop_gen_map(const Geo& g, const Rules& rl, const Tables* tab, Row4<MAXW>& rw,
+                                    uint32_t env_id, uint32_t episode, int lane) {
+  const int G = g.G, R = g.R;
+  const bool own = lane < G;
+  uint64_t real[MAXW];
+#pragma unroll
+  for (int w = 0; w < MAXW; ++w) {
+    const bool in = MAXW == 1 || w < g.WPR;
+    real[w] = in ? tab->grid_real[w] : 0ull;
+    rw.set(w, own && in ? tab->grid_pad[w] : 0ull);
+  }
+  WaveStream rng;
+  rng.init(rl.seed, env_id, episode, lane);
+  // obstacle clusters, plantos_env.py:341-354
+  const int clusters = rl.O / 3;
+  for (int q = 0; q < clusters; ++q) {
+    const int cx = 2 + (int)rng.below((uint32_t)(G - 4), lane);
+    const int cy = 2 + (int)rng.below((uint32_t)(G - 4), lane);
+    const int size = 2 + (int)rng.below(2u, lane);
+    const int x0 = cx - size / 2;
+    if (own && lane >= x0 && lane < x0 + size)
+      for (int dy = 0; dy < size; ++dy) {
+        const int oy = cy + dy - size / 2;
+        if (0 <= oy && oy < G) coop_set(rw, oy + R, OBST);
+      }
+  }
+  int c0 = 0, nob = 0;
+#pragma unroll
+  for (int w = 0; w < MAXW; ++w) {
+    const uint64_t v = rw.get(w), rl_w = own ? real[w] : 0ull;
+    nob += __popcll(v & ~(v >> 1) & rl_w & kEven64);
+    c0 += __popcll(cand_mask(v, rl_w, 0));
+  }
+  const int nfree = g.GG - wave_sum(nob);
+  Scal s;
+  s.step = 0;
+  s.coll = 0;
+  s.flags = 0;
+  s.episode = episode + 1u;
+  s.total = nfree;
+  s.expl = 1;
+  if (nfree < rl.P + 1) {  // ValueError, plantos_env.py:360-364
+    s.flags = F_NOROOM;
+    s.x = 0;
+    s.y = 0;
+    s.expl = 0;
+    return s;
+  }
+  // random.sample(list(available), P): plants are not obstacles, so the kind-0
+  // counts stay valid for every pick; a pick of an already chosen cell redraws.
+  // Pick i is kept in lane i % 64 (registers pk0 / pk1).
+  const int i0 = wave_incl_scan(c0, lane), e0 = i0 - c0;
+  int pk0 = 0, pk1 = 0;
+  for (int i = 0; i < rl.P; ++i) {
+    int row, pcol;
+    for (;;) {
+      coop_nth_cell(rw, g.WPR, real, i0, e0, (int)rng.below((uint32_t)nfree, lane), 0, lane, row, pcol);
+      const uint64_t word = readlane64(rw.get((2 * pcol) >> 6), row);
+      if (((word >> ((2 * pcol) & 63)) & 3u) == EMPTY) break;
+    }
+    if (lane == row) coop_set(rw, pcol, HYD);
+    const int cell = row * G + pcol - R;
+    if (lane == (i & 63)) {
+      if (i < 64) pk0 = cell;
+      else pk1 = cell;
+    }
+  }
+  // thirsty draws in sample order, plantos_env.py:367-369
+  for (int i = 0; i < rl.P; ++i) {
+    const int c = __builtin_amdgcn_readlane(i < 64 ? pk0 : pk1, i & 63);
+    if (rng.random53(lane) < rl.p_thirsty && lane == c / G) coop_set(rw, c % G + R, THIRSTY);
+  }
+  // rover: choice(list(available - plants)), plantos_env.py:370-372
+  int c1 = 0;
+#pragma unroll
+  for (int w = 0; w < MAXW; ++w) c1 += __popcll(cand_mask(rw.get(w), own ? real[w] : 0ull, 1));
+  const int i1 = wave_incl_scan(c1, lane);
+  int row, pcol;
+  coop_nth_cell(rw, g.WPR, real, i1, i1 - c1, (int)rng.below((uint32_t)(nfree - rl.P), lane), 1, lane, row, pcol);
+  s.x = row;
+  s.y = pcol - R;
+  return s;
+}
+
+// _get_info (plantos_env.py:317-336) of env e's current state by one wave
+// (write_info's columns); s: the env's scalars (uniform).
+__device__ inline void coop_write_info(const State& st, const Geo& g, int64_t e, const Scal& s, int32_t* o, int lane) {
+  int th = 0, hy = 0;
+  if (lane < g.G)
+    for (int w = 0; w < g.WPR; ++w) {
+      // sc1 load (L2): the row may hold a word another lane of this wave just stored
+      const uint64_t v = __hip_atomic_load(st.grid + e * g.gstride + (int64_t)lane * g.WPR + w, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t lo = v & kEven64, hi = (v >> 1) & kEven64, real = st.tab->grid_real[w];
+      th += __popcll(lo & hi & real);   // sum(plants.values())     :318
+      hy += __popcll(~lo & hi & real);  // len(plants) - thirsty    :319
+    }
+  th = wave_sum(th);
+  hy = wave_sum(hy);
+  int v = 0;
+  switch (lane) {
+    case 0: v = s.x; break;                             // rover_position     :324
+    case 1: v = s.y; break;
+    case 2: v = th; break;
+    case 3: v = hy; break;
+    case 4: v = th + hy; break;                         // total_plants       :327
+    case 5: v = s.step; break;                          // step_count         :328
+    case 6: v = s.expl; break;                          // explored_cells     :320
+    case 7: v = s.total; break;                         // total_cells        :321
+    case 8: v = (s.flags & F_COLLIDED) ? 1 : 0; break;  // collided_with_wall :333
+    case 9: v = s.coll; break;                          // total_collisions   :334
+    case 10: v = (int)((s.flags >> 2) & 7u); break;     // error flags (PE_S_POISONED layout)
+    default: break;
+  }
+  if (lane < PE_NINFO) o[lane] = v;
+}
+
+// reset() of env e (plantos_env.py:125-158) by one wave: map, grid rows and visit
+// rows to HBM (lane r writes row r), the curriculum's carried-visits mode as
+// new_episode_visits.  keep: CurriculumWrapper keeps the previous visit counts.
+template <int MAXW>
+__device__ inline Scal coop_reset_env(const State& st, const Geo& g, const Rules& rl, int64_t e, uint32_t episode,
+                                      bool keep, Row4<MAXW>& rw, int lane) {
+  const Tables* tab = st.tab;
+  Scal s = coop_gen_map<MAXW>(g, rl, tab, rw, rl.env_off + (uint32_t)e, episode, lane);
+  if ((s.flags & F_NOROOM) && lane == 0) atomicOr(st.err_bits, F_NOROOM);
+  if (lane < g.G) {
+    uint64_t* gb = st.grid + e * g.gstride + (int64_t)lane * g.WPR;
+#pragma unroll
+    for (int w = 0; w < MAXW; ++w)
+      if (MAXW == 1 || w < g.WPR) gb[w] = rw.get(w);
+  }
+  if (!keep) {  // reset_visits: all zero (pads 10), visit[rover] = 1 (:146-147)
+    if (lane < g.G) {
+      uint32_t* vb = st.vis + e * g.vstride + (int64_t)lane * g.NW;
+      const int bit = 4 * (s.y + 2);
+      const bool rover = lane == s.x && !(s.flags & F_NOROOM);
+      for (int w = 0; w < g.NW; ++w) {
+        uint32_t v = tab->vis_pad[w];
+        if (rover && w == (bit >> 5)) v = (v & ~(0xFu << (bit & 31))) | (1u << (bit & 31));
+        vb[w] = v;
+      }
+    }
+  } else {  // explored map restarted at the rover, bitmap mode (new_episode_visits)
+    const int rc = s.x * g.G + s.y;
+    for (int w = lane; w < g.estride; w += 64)
+      st.expl[e * g.estride + w] = (!(s.flags & F_NOROOM) && w == (rc >> 5)) ? (1u << (rc & 31)) : 0u;
+    s.flags |= F_EXPL_BITMAP;
+  }
+  return s;
+}
+
+// build_obs_fresh by one wave from the rows in the lanes' registers: lane i
+// marches ray i (plantos_env.py:260-292), lanes 0..26 the position and the 5x5
+// slice of a fresh episode (visit 1 at the rover, :294-313).  out: the env's obs
+// row (LDS tile row or HBM); ldx/ldy: the handle's LIDAR offset tables.
+template <int MAXW>
+__device__ inline void coop_fresh_obs(const Geo& g, const Row4<MAXW>& rw, const Scal& s, float* out,
+                                      const float* tdist, const float* tpos, const float* tvis,
+                                      const signed char* ldx, const signed char* ldy, int lane) {
+  const int R = g.R, C = g.C, G = g.G;
+  // every lane takes part in every row fetch (a lane that left the loop could not
+  // serve its row to the others): first hits are latched, not broken out of
+  const int li = lane < C ? lane : 0;
+  int dist = R, ent = EMPTY;
+  bool hit = false;
+  for (int r = 1; r <= R; ++r) {
+    const int cx = s.x + ldx[li * R + r - 1];
+    const int cy = s.y + ldy[li * R + r - 1];
+    const bool inr = cx >= 0 && cx < G;
+    const int src = inr ? cx : 0;
+    const int bit = 2 * (cy + R);
+    Row4<MAXW> fetched{0ull, 0ull, 0ull, 0ull};
+#pragma unroll
+    for (int w = 0; w < MAXW; ++w)
+      if (MAXW == 1 || w < g.WPR) fetched.set(w, shfl64(rw.get(w), src));
+    const uint64_t word = fetched.get(bit >> 6);
+    const int code = inr ? (int)((word >> (bit & 63)) & 3u) : OBST;  // :271-284
+    if (!hit && code != EMPTY) {
+      hit = true;
+      dist = r;
+      ent = code;
+    }
+  }
+  if (lane < C) {
+    out[5 * lane] = tdist[dist];
+    out[5 * lane + 1] = ent == 0 ? 1.0f : 0.0f;
+    out[5 * lane + 2] = ent == 1 ? 1.0f : 0.0f;
+    out[5 * lane + 3] = ent == 2 ? 1.0f : 0.0f;
+    out[5 * lane + 4] = ent == 3 ? 1.0f : 0.0f;
+  }
+  if (lane < 25) {
+    const int lx = lane / 5, ly = lane % 5;
+    const int gx = s.x + lx - 2, gy = s.y + ly - 2;
+    const bool in = gx >= 0 && gx < G && gy >= 0 && gy < G;  // :307-311
+    const bool rover = lane == 12 && !(s.flags & F_NOROOM);
+    out[5 * C + 2 + lane] = !in ? tvis[10] : (rover ? tvis[1] : tvis[0]);
+  } else if (lane < 27) {
+    out[5 * C + lane - 25] = tpos[lane == 25 ? s.x : s.y];  // :294-296
+  }
+}
+
+}  // namespace pe

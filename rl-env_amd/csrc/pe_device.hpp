@@ -102,6 +102,7 @@ struct Rules {
   double cur_max, cur_inc;  // CurriculumWrapper max_threshold, threshold_increment
   int cur_max_eps;          // max_episodes_per_maze (A2C_training.py:54)
   int map_algo;             // PE_MAP_ORIGINAL / PE_MAP_MAZE (the fork, plantos_env_new.py:355-358)
+  int coop_max_done;        // step kernel: wave-cooperative resets up to this many done envs per block
 };
 
 // CurriculumWrapper.step (A2C_training.py:97-109): exploration_percentage >= the
@@ -478,7 +479,7 @@ __device__ inline void maze_obstacles(const Geo& g, const Tables* tab, uint64_t*
 // image sg (all rows) and returns the new scalars of the episode (flags F_NOROOM
 // if there is no room, plantos_env.py:360-364).  picks: max(2P,
 // maze_scratch_bytes(G)) bytes of scratch.
-__device__ inline Scal gen_map(const Geo& g, const Rules& rl, const Tables* tab, uint64_t* sg, uint16_t* picks,
+__device__ __forceinline__ Scal gen_map(const Geo& g, const Rules& rl, const Tables* tab, uint64_t* sg, uint16_t* picks,
                                uint32_t env_id, uint32_t episode) {
   const int G = g.G;
   Stream rng;
@@ -568,7 +569,7 @@ __device__ inline void new_episode_visits(const State& st, const Geo& g, const T
 
 // reset() for one env (plantos_env.py:125-158), generated in place in HBM.
 // tab: the handle's tables, ideally a copy in LDS (read in every scan step).
-__device__ inline Scal reset_env(const State& st, const Geo& g, const Rules& rl, const Tables* tab, int64_t e,
+__device__ __forceinline__ Scal reset_env(const State& st, const Geo& g, const Rules& rl, const Tables* tab, int64_t e,
                                  uint32_t episode) {
   const bool keep = st.cur ? curriculum_on_reset(st.cur, e, rl) : false;
   uint16_t* picks = reinterpret_cast<uint16_t*>(st.vx + e * g.hstride);  // scratch (all nibbles 0 after)
@@ -589,7 +590,7 @@ __host__ __device__ constexpr int reset_scratch_bytes(int G, int WPR, int P) {
 
 // reset() generated in a scratch image (LDS) and written to HBM row by row:
 // the rejection-sampling scans run at LDS latency instead of HBM latency.
-__device__ inline Scal reset_env_scratch(const State& st, const Geo& g, const Rules& rl, const Tables* tab, int64_t e,
+__device__ __forceinline__ Scal reset_env_scratch(const State& st, const Geo& g, const Rules& rl, const Tables* tab, int64_t e,
                                          uint32_t episode, uint64_t* sg) {
   const bool keep = st.cur ? curriculum_on_reset(st.cur, e, rl) : false;
   uint16_t* picks = reinterpret_cast<uint16_t*>(sg + g.G * g.WPR);

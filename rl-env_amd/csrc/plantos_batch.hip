@@ -21,6 +21,7 @@
 #include "lidar_tables.inc"
 #include "pe_device.hpp"
 #include "pe_fast.hpp"
+#include "pe_coop.hpp"
 #include "pe_quad.hpp"
 
 using namespace pe;
@@ -526,8 +527,149 @@ constexpr int quad_tile_off() {
   return (kTabFloats + (2 * R + 3) * kQuadEnvs * 2 + 7 * kQuadEnvs + 3) & ~3;
 }
 
+// ---- pe_step_quad's auto-reset slow path (a block with a done env), out of line:
+// kept in separate functions so that their register demand (map generation, the
+// cooperative reset) does not raise the hot path's.  `ka` is the kernel's
+// argument segment (StepArgs); LDS is the kernel's dynamic LDS (same layout).
+// the kernel's argument segment as a generic pointer (constant and global
+// addresses coincide in the flat space)
+__device__ __forceinline__ const void* kernargs() {
+  return reinterpret_cast<const void*>(reinterpret_cast<uintptr_t>(__builtin_amdgcn_kernarg_segment_ptr()));
+}
+
+__device__ __forceinline__ bool quad_coop(const StepArgs& a, int ndone) {
+#ifdef PE_NO_COOP
+  return false;
+#else
+  return a.autoreset && ndone <= a.rl.coop_max_done;
+#endif
+}
+
+template <int NW, bool ONEWORD>  // one copy per kernel: each inherits its kernel's register budget
+__device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, int C, int R, int lane, int wv, int CW,
+                                                int64_t e0, bool done, uint4 sp, double ret, int ndone) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const StepArgs& a = *reinterpret_cast<const StepArgs*>(ka);
+  const Geo& g = a.g;
+  const Rules& rl = a.rl;
+  const State& st = a.st;
+  float* tdist = smem;
+  float* tpos = smem + 72;
+  float* tvis = smem + 328;
+  const Tables* ltab = reinterpret_cast<const Tables*>(smem);
+  uint64_t* lrow = reinterpret_cast<uint64_t*>(smem + kTabFloats);
+  float* rows = smem + tile_off;
+  float* row = rows + lane * g.D;
+  const int64_t e = e0 + lane;
+  Scal s = unpack(sp);
+  if (quad_coop(a, ndone)) {
+    // A few done envs: wave-cooperative resets (pe_coop.hpp).  The commit wave
+    // walks its done envs; for each, all 64 lanes copy the terminal obs row, write
+    // the terminal info, generate the map, write grid + visit rows and build the
+    // fresh obs into the env's tile row, which the tile store then streams out.
+    bool keep = false;
+    if (done) {
+      if (a.ep_ret_out) a.ep_ret_out[e] = ret;
+      if (a.ep_len_out) a.ep_len_out[e] = s.step;
+      if (st.cur) keep = curriculum_on_reset(st.cur, e, rl);  // A2C_training.py:56-95
+    }
+    if (wv == CW) {
+      constexpr int MAXW = ONEWORD ? 1 : kCoopWPR;
+      // the commit's grid stores (watering) must have landed before other lanes
+      // read the env's rows for its terminal info
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      uint64_t dm = __ballot(done);
+      while (dm) {
+        const int l = __ffsll((unsigned long long)dm) - 1;
+        dm &= dm - 1;
+        const int64_t el = e0 + l;
+        float* orow = rows + l * g.D;
+        if (a.tobs) {
+          float* t = a.tobs + el * g.D;
+          for (int k = lane; k < g.D; k += 64) t[k] = orow[k];
+        }
+        const uint4 sl = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)sp.x, l),
+                                    (uint32_t)__builtin_amdgcn_readlane((int)sp.y, l),
+                                    (uint32_t)__builtin_amdgcn_readlane((int)sp.z, l),
+                                    (uint32_t)__builtin_amdgcn_readlane((int)sp.w, l));
+        const Scal sv = unpack(sl);
+        if (a.tinfo) coop_write_info(st, g, el, sv, a.tinfo + el * PE_NINFO, lane);
+        const bool kp = __builtin_amdgcn_readlane((int)keep, l) != 0;
+        Row4<MAXW> rw;
+        const Scal ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane);
+        asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
+        coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
+        if (lane == l) s = ns;
+      }
+      if (done) {
+        st.ep_ret[e] = 0.0;
+        st.scal[e] = pack(s);
+      }
+    }
+    __syncthreads();  // fresh tile rows complete before the tile store
+    return pack(s);
+  }
+  // Many done envs (a synchronized batch truncating together): one lane per env.
+  // The done env's own obs-tile row is free once its terminal obs is copied out:
+  // the new map is generated there when it can hold the grid image (LDS latency
+  // for the rejection-sampling scans; the fresh obs row goes straight to HBM
+  // after the tile store, quad_done_obs)
+  const bool scratch_ok = reset_scratch_bytes(g.G, g.WPR, rl.P) <= 4 * g.D;
+  // 8-B aligned start inside the row (rows is 16-B aligned, D is odd)
+  uint64_t* sg = reinterpret_cast<uint64_t*>(row + ((lane * g.D) & 1));
+  // LIDAR offsets for the reset-path obs builders, staged in the (now dead) window region
+  const signed char* lldx = reinterpret_cast<const signed char*>(lrow);
+  const signed char* lldy = lldx + C * R;
+  PE_RSTAMP(0);
+  load_tables_cold(smem, st.tab);
+  for (int k = threadIdx.x; k < C * R; k += blockDim.x) {
+    reinterpret_cast<signed char*>(lrow)[k] = st.ldx[k];
+    reinterpret_cast<signed char*>(lrow)[C * R + k] = st.ldy[k];
+  }
+  __syncthreads();
+  if (done) {
+    if (a.tobs) {
+      float* t = a.tobs + e * g.D;
+      for (int k = 0; k < g.D; ++k) t[k] = row[k];
+    }
+    if (a.ep_ret_out) a.ep_ret_out[e] = ret;
+    if (a.ep_len_out) a.ep_len_out[e] = s.step;
+    PE_RSTAMP(1);
+    if (a.tinfo) write_info(a.st, a.g, ltab, e, s, a.tinfo + e * PE_NINFO);
+    PE_RSTAMP(2);
+    if (!a.autoreset) {
+    } else if (scratch_ok) {
+      s = reset_env_scratch(st, g, rl, ltab, e, s.episode, sg);
+      PE_RSTAMP(3);
+    } else {
+      s = reset_env(st, g, rl, ltab, e, s.episode);
+      build_obs_fresh(a, st.grid + e * g.gstride, s, row, tdist, tpos, tvis, lldx, lldy);
+    }
+    if (a.autoreset) {
+      st.ep_ret[e] = 0.0;
+      st.scal[e] = pack(s);
+    }
+  }
+  __syncthreads();
+  return pack(s);
+}
+
+// The lane-per-env path's fresh obs, after the tile store (see quad_done_path).
+template <int NW>
+__device__ __forceinline__ void quad_done_obs(const void* ka, int tile_off, int lane, int64_t e, bool done, uint4 sp) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const StepArgs& a = *reinterpret_cast<const StepArgs*>(ka);
+  const Geo& g = a.g;
+  float* row = smem + tile_off + lane * g.D;
+  const uint64_t* sg = reinterpret_cast<const uint64_t*>(row + ((lane * g.D) & 1));
+  const signed char* lldx = reinterpret_cast<const signed char*>(smem + kTabFloats);
+  PE_RSTAMP(4);
+  if (done) build_obs_fresh(a, sg, unpack(sp), a.obs + e * g.D, smem, smem + 72, smem + 328, lldx, lldx + g.C * g.R);
+  PE_RSTAMP(5);
+}
+
 template <int C, int R, bool ONEWORD, int NW>
-__global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs
   constexpr int NR = 2 * R + 3, NV = 7, EPB = kQuadEnvs, CW = NW - 1;  // CW: commit wave
   static_assert(C % NW == 0, "rays must split evenly over the waves");
   static_assert(ONEWORD || R <= 14, "funnel-shifted window row must hold 2R+5 cells");
@@ -808,63 +950,24 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
   }
   PE_STAMP(4);
   // ---- DummyVecEnv auto-reset (rare): commit wave, after the whole obs row is in LDS
-  const int any_done = __syncthreads_or(done);
+  const int ndone = __syncthreads_count(done);  // done envs of the block (0: the usual case)
+  const bool any_done = ndone > 0;
   PE_STAMP(5);
-  // The done env's own obs-tile row is free once its terminal obs is copied out:
-  // when it can hold the grid image, the new map is generated there (LDS latency
-  // for the rejection-sampling scans) and the fresh obs row goes straight to HBM
-  // after the tile store.
-  const bool scratch_ok = reset_scratch_bytes(g.G, g.WPR, rl.P) <= 4 * g.D;
-  // 8-B aligned start inside the row (rows is 16-B aligned, D is odd); pointer
-  // arithmetic keeps the LDS address space visible to the compiler (ds_* ops)
-  uint64_t* sg = reinterpret_cast<uint64_t*>(row + ((lane * g.D) & 1));
-  // LIDAR offsets for the reset-path obs builders, staged in the (now dead) window region
-  static_assert(2 * C * R <= (NR * 8 + NV * 4) * EPB, "offset tables must fit the window region");
-  const signed char* lldx = reinterpret_cast<const signed char*>(lrow);
-  const signed char* lldy = lldx + C * R;
+  // auto-reset slow path, out of line (its registers stay off the hot path)
+  static_assert(2 * C * R <= (NR * 8 + NV * 4) * EPB, "LIDAR offset tables must fit the window region");
   if (any_done) {
-    PE_RSTAMP(0);
-    load_tables_cold(smem, st.tab);
-    for (int k = threadIdx.x; k < C * R; k += blockDim.x) {
-      reinterpret_cast<signed char*>(lrow)[k] = st.ldx[k];
-      reinterpret_cast<signed char*>(lrow)[C * R + k] = st.ldy[k];
-    }
-    __syncthreads();
-    if (done) {
-      if (a.tobs) {
-        float* t = a.tobs + e * g.D;
-        for (int k = 0; k < g.D; ++k) t[k] = row[k];
-      }
-      if (a.ep_ret_out) a.ep_ret_out[e] = ret;
-      if (a.ep_len_out) a.ep_len_out[e] = s.step;
-      PE_RSTAMP(1);
-      if (a.tinfo) write_info(a.st, a.g, ltab, e, s, a.tinfo + e * PE_NINFO);
-      PE_RSTAMP(2);
-      if (!a.autoreset) {
-      } else if (scratch_ok) {
-        s = reset_env_scratch(st, g, rl, ltab, e, s.episode, sg);
-        PE_RSTAMP(3);
-      } else {
-        s = reset_env(st, g, rl, ltab, e, s.episode);
-        build_obs_fresh(a, st.grid + e * g.gstride, s, row, tdist, tpos, tvis, lldx, lldy);
-      }
-      if (a.autoreset) {
-        st.ep_ret[e] = 0.0;
-        st.scal[e] = pack(s);
-      }
-    }
-    __syncthreads();
+    const uint4 ns = quad_done_path<NW, ONEWORD>(kernargs(), quad_tile_off<R>(), C, R, lane, wv, CW, e0, done,
+                                                 pack(s), ret, ndone);
+    s = unpack(ns);
   }
   const int64_t valid = a.n - e0 < EPB ? a.n - e0 : EPB;
   if constexpr (!(kAblate & 1)) store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D);
-  if (any_done && scratch_ok && a.autoreset) {
+  if (any_done && a.autoreset && !quad_coop(a, ndone) && reset_scratch_bytes(g.G, g.WPR, rl.P) <= 4 * g.D) {
     // the tile store above wrote scratch bytes into the done rows: drain it, then
     // overwrite those rows with the fresh obs built from the LDS grid image
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    PE_RSTAMP(4);
-    if (done) build_obs_fresh(a, sg, s, a.obs + e * g.D, tdist, tpos, tvis, lldx, lldy);
-    PE_RSTAMP(5);
+    quad_done_obs<NW>(kernargs(), quad_tile_off<R>(), lane, e, done, pack(s));
   }
   PE_STAMP(6);
 #ifdef PE_STAMPS
@@ -1360,6 +1463,19 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   rl.P = P;
   rl.O = O;
   rl.map_algo = c->map_generation_algo;
+  // Auto-resets in the step kernel: wave-cooperative (pe_coop.hpp: one env at a
+  // time per wave, ~10 us each at 20x20) when a block has few done envs; one lane
+  // per env (all of a wave's envs at once, ~0.26 ms for a whole batch at 20x20)
+  // when many are done together -- unless the lane path would have to scan its
+  // grid image in HBM (no room for it in the obs-tile row), where it is ~30x
+  // slower (29 ms for a whole 64x64 batch) and the cooperative path always wins.
+  if (!coop_reset_ok(G, g.WPR, g.NW, P, C, c->map_generation_algo))
+    rl.coop_max_done = 0;
+  else if (reset_scratch_bytes(G, g.WPR, P) <= 4 * g.D)
+    rl.coop_max_done = kCoopMaxDone;
+  else
+    rl.coop_max_done = kQuadEnvs;
+  if (const char* cm = std::getenv("PE_COOP_MAX_DONE")) rl.coop_max_done = std::atoi(cm);  // A/B
   rl.max_steps = c->max_steps;
 
   // host tables
@@ -1399,7 +1515,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   h->kname = variant_name(h->variant);
   const char* qw = std::getenv("PE_QUAD_WAVES");
   // measured (profiles/r1c-r1e): 4 waves win at C=16, 8 waves at C=64
-  h->quad_waves = qw ? (std::atoi(qw) == 4 ? 4 : 8) : (C >= 64 ? 8 : 4);
+  h->quad_waves = qw ? (std::atoi(qw) == 8 ? 8 : 4) : 4;  // 4 measured best at C=16 and C=64
   const char* sg = std::getenv("PE_STAGGER");
   h->stagger = sg ? std::atoi(sg) : 0;
   const char* lf = std::getenv("PE_LDS_FLOOR");

@@ -1,0 +1,136 @@
+"""GPU parity of the step kernel's auto-reset paths against the oracle with
+DESYNCHRONIZED episodes (every env starts at its own step count, so a few envs
+reset in every step, as in steady-state training): the wave-cooperative reset
+(pe_coop.hpp: sparse resets, and every reset at 64x64) and, forced through
+PE_COOP_MAX_DONE, both paths for dense resets.  Every output of every step is
+compared, plus the terminal info rows and the final state.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from oracle_rollout import OracleVec
+
+pytestmark = pytest.mark.gpu
+
+CFG = {
+    "g20": (20, 10, 12, 6, 16),
+    "g64": (64, 100, 120, 6, 64),
+    "g7": (7, 3, 3, 3, 12),
+    "g32": (32, 20, 30, 9, 24),
+    "g21": (21, 8, 50, 2, 10),
+}
+
+
+def np_(t):
+    return t.detach().cpu().numpy()
+
+
+def info_rows(b, idx):
+    rows = np.zeros((len(idx), 11), np.int32)
+    for k, e in enumerate(idx):
+        th, hy, tot, ex, tc = b.info(e)
+        s = b.scal[e]
+        rows[k] = [s[O.S_X], s[O.S_Y], th, hy, tot, s[O.S_STEP], ex, tc, s[O.S_COLLIDED], s[O.S_COLL], s[O.S_POISONED]]
+    return rows
+
+
+@pytest.mark.parametrize("name,n,steps,spread,coop_max", [
+    ("g20", 2048, 160, 150, None),   # sparse: cooperative resets
+    ("g64", 192, 50, 40, None),      # 64x64: cooperative resets always
+    ("g7", 700, 120, 100, None),
+    ("g32", 300, 60, 50, None),
+    ("g21", 400, 60, 50, None),
+    ("g20", 256, 12, 1, "64"),       # every env at once, forced through the cooperative path
+    ("g64", 128, 12, 1, "0"),        # every env at once, forced through the lane-per-env path
+])
+def test_desync_autoreset_parity(name, n, steps, spread, coop_max, monkeypatch):
+    from plantos_amd import PlantOSBatch
+    if coop_max is not None:
+        monkeypatch.setenv("PE_COOP_MAX_DONE", coop_max)
+    G, P, Ob, R, C = cfg = CFG[name]
+    seed = 31
+    b = PlantOSBatch(n, grid_size=G, num_plants=P, num_obstacles=Ob, lidar_range=R, lidar_channels=C, seed=seed,
+                     device="cuda:0")
+    ov = OracleVec(cfg, np.arange(n), seed)
+    # desynchronize: env e starts at step 1000 - 1 - k(e), k in [0, spread)
+    rng = np.random.default_rng(5)
+    start = (999 - rng.integers(0, spread, n)).astype(np.int32)
+    sc = np_(b.get_state()["scalars"])
+    sc[:, O.S_STEP] = start
+    b.set_state(scalars=sc)
+    ov.b.scal[:, O.S_STEP] = start
+    act = torch.empty(n, dtype=torch.int32, device="cuda:0")
+    resets = 0
+    for t in range(steps):
+        b.synth_actions(seed, t, out=act)
+        a_np = np_(act)
+        obs, rew, te, tr = b.step(act)
+        # oracle: step, pre-reset info of the done envs, then the resets (OracleVec.step)
+        o_obs, o_rew, o_te, o_tr = ov.b.step(a_np)
+        done = o_te | o_tr
+        didx = np.nonzero(done)[0]
+        o_info = info_rows(ov.b, didx)
+        o_tobs = o_obs.copy()
+        ov.ret += o_rew
+        o_ret, o_len = ov.ret.copy(), ov.b.scal[:, O.S_STEP].copy()
+        for k in didx:
+            ov.b.reset_philox(int(k), seed, int(k), int(ov.b.scal[k, O.S_EPISODE]))
+            ov.ret[k] = 0.0
+        if len(didx):
+            o_obs[done] = ov.b.obs(didx)[done]
+        resets += len(didx)
+        assert (np_(rew) == o_rew.astype(np.float32)).all(), t
+        assert (np_(te).astype(bool) == o_te).all() and (np_(tr).astype(bool) == o_tr).all(), t
+        assert (np_(obs) == o_obs).all(), t
+        if len(didx):
+            assert (np_(b.terminal_obs)[didx] == o_tobs[didx]).all(), t
+            assert (np_(b.episode_return)[didx] == o_ret[didx]).all(), t
+            assert (np_(b.episode_length)[didx] == o_len[didx]).all(), t
+            assert (np_(b.terminal_info)[didx] == o_info).all(), t
+    assert resets >= n  # every env reset at least once
+    st = b.get_state()
+    assert (np_(st["cells"]) == ov.b.cells).all()
+    assert (np_(st["visits"]) == ov.b.visits).all()
+    assert (np_(st["scalars"]) == ov.b.scal).all()
+    b.close()
+
+
+def test_desync_curriculum_cooperative_reset():
+    """CurriculumWrapper (visit counts carried into the next episode, explored map
+    restarted) through the cooperative reset: state after sparse resets equals the
+    lane-per-env path's (PE_COOP_MAX_DONE=0) on the same inputs."""
+    from plantos_amd import PlantOSBatch
+    import os
+    G, P, Ob, R, C = CFG["g20"]
+    n, steps = 512, 60
+    outs = []
+    for cm in ("8", "0"):
+        os.environ["PE_COOP_MAX_DONE"] = cm
+        try:
+            b = PlantOSBatch(n, grid_size=G, num_plants=P, num_obstacles=Ob, lidar_range=R, lidar_channels=C,
+                             seed=3, device="cuda:0")
+        finally:
+            del os.environ["PE_COOP_MAX_DONE"]
+        b.enable_curriculum(initial_threshold=5.0, max_threshold=100.0)
+        sc = np_(b.get_state()["scalars"])
+        sc[:, O.S_STEP] = 999 - np.random.default_rng(2).integers(0, 50, n)
+        b.set_state(scalars=sc)
+        act = torch.empty(n, dtype=torch.int32, device="cuda:0")
+        trace = []
+        for t in range(steps):
+            b.synth_actions(3, t, out=act)
+            obs, rew, te, tr = b.step(act)
+            trace.append((np_(obs).copy(), np_(rew).copy(), np_(te).copy(), np_(tr).copy()))
+        st = {k: np_(v).copy() for k, v in b.get_state().items()}
+        outs.append((trace, st, [np_(x).copy() for x in b.get_curriculum()]))
+        b.close()
+    (ta, sa, ca), (tb, sb, cb) = outs
+    for x, y in zip(ta, tb):
+        for u, v in zip(x, y):
+            assert (u == v).all()
+    for k in sa:
+        assert (sa[k] == sb[k]).all(), k
+    for u, v in zip(ca, cb):
+        assert (u == v).all()
