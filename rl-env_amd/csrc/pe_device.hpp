@@ -102,7 +102,6 @@ struct Rules {
   double cur_max, cur_inc;  // CurriculumWrapper max_threshold, threshold_increment
   int cur_max_eps;          // max_episodes_per_maze (A2C_training.py:54)
   int map_algo;             // PE_MAP_ORIGINAL / PE_MAP_MAZE (the fork, plantos_env_new.py:355-358)
-  int coop_max_done;        // step kernel: wave-cooperative resets up to this many done envs per block
 };
 
 // CurriculumWrapper.step (A2C_training.py:97-109): exploration_percentage >= the

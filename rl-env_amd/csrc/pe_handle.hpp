@@ -19,6 +19,7 @@ struct pe_handle {
   size_t lds_floor;  // PE_LDS_FLOOR (diagnostics): minimum dynamic LDS per step workgroup
   int quad_waves;    // waves per workgroup of the sector kernel (4 or 8; PE_QUAD_WAVES)
   int stagger;       // PE_STAGGER (experimental): sector-kernel start delay per block quarter
+  int coop_max_done; // wave-cooperative auto-resets up to this many done envs per block (pe_coop.hpp)
 };
 
 // pe_internal_set_error (plantos_batch.hip): records pe_last_error() for this thread.

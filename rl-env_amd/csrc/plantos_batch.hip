@@ -39,6 +39,7 @@ struct StepArgs {
   int n;
   int autoreset;
   int act_bytes;
+  int coop_max_done;  // step kernel: wave-cooperative resets up to this many done envs per block
   const void* actions;
   float* obs;
   float* reward;
@@ -541,7 +542,7 @@ __device__ __forceinline__ bool quad_coop(const StepArgs& a, int ndone) {
 #ifdef PE_NO_COOP
   return false;
 #else
-  return a.autoreset && ndone <= a.rl.coop_max_done;
+  return a.autoreset && ndone <= a.coop_max_done;
 #endif
 }
 
@@ -563,50 +564,77 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
   const int64_t e = e0 + lane;
   Scal s = unpack(sp);
   if (quad_coop(a, ndone)) {
-    // A few done envs: wave-cooperative resets (pe_coop.hpp).  The commit wave
-    // walks its done envs; for each, all 64 lanes copy the terminal obs row, write
-    // the terminal info, generate the map, write grid + visit rows and build the
-    // fresh obs into the env's tile row, which the tile store then streams out.
-    bool keep = false;
-    if (done) {
-      if (a.ep_ret_out) a.ep_ret_out[e] = ret;
-      if (a.ep_len_out) a.ep_len_out[e] = s.step;
-      if (st.cur) keep = curriculum_on_reset(st.cur, e, rl);  // A2C_training.py:56-95
-    }
+    // A few done envs: wave-cooperative resets (pe_coop.hpp), spread over the
+    // block's waves (the k-th done env to wave k % NW).  For each, the 64 lanes
+    // copy the terminal obs row out, write the terminal info, generate the map,
+    // write grid + visit rows and build the fresh obs into the env's tile row,
+    // which the tile store then streams out with the others.  The commit wave
+    // stages each done env's scalars in the (dead) window region of LDS and
+    // stores the new ones afterwards: every store to an env's scalars stays in
+    // its own lane, in program order.
+    uint32_t* stage = reinterpret_cast<uint32_t*>(lrow);  // [64][5]: packed scalars, keep
+    uint64_t* dmask = reinterpret_cast<uint64_t*>(stage + 5 * kQuadEnvs);
+    const int NWv = blockDim.x >> 6;
     if (wv == CW) {
-      constexpr int MAXW = ONEWORD ? 1 : kCoopWPR;
-      // the commit's grid stores (watering) must have landed before other lanes
-      // read the env's rows for its terminal info
+      bool keep = false;
+      if (done) {
+        if (a.ep_ret_out) a.ep_ret_out[e] = ret;
+        if (a.ep_len_out) a.ep_len_out[e] = s.step;
+        if (st.cur) keep = curriculum_on_reset(st.cur, e, rl);  // A2C_training.py:56-95
+        stage[5 * lane] = sp.x;
+        stage[5 * lane + 1] = sp.y;
+        stage[5 * lane + 2] = sp.z;
+        stage[5 * lane + 3] = sp.w;
+        stage[5 * lane + 4] = keep;
+      }
+      const uint64_t dm = __ballot(done);
+      if (lane == 0) *dmask = dm;
+      // the commit's grid stores (watering) must land before other waves read
+      // the env's rows for its terminal info
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      uint64_t dm = __ballot(done);
-      while (dm) {
+    }
+    __syncthreads();
+    {
+      constexpr int MAXW = ONEWORD ? 1 : kCoopWPR;
+      const uint64_t dml = *dmask;  // uniform: read into scalar registers
+      uint64_t dm = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)dml) |
+                    ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(dml >> 32)) << 32);
+      for (int k = 0; dm; ++k) {
         const int l = __ffsll((unsigned long long)dm) - 1;
         dm &= dm - 1;
+        if (k % NWv != wv) continue;
         const int64_t el = e0 + l;
         float* orow = rows + l * g.D;
         if (a.tobs) {
           float* t = a.tobs + el * g.D;
-          for (int k = lane; k < g.D; k += 64) t[k] = orow[k];
+          for (int k2 = lane; k2 < g.D; k2 += 64) t[k2] = orow[k2];
         }
-        const uint4 sl = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)sp.x, l),
-                                    (uint32_t)__builtin_amdgcn_readlane((int)sp.y, l),
-                                    (uint32_t)__builtin_amdgcn_readlane((int)sp.z, l),
-                                    (uint32_t)__builtin_amdgcn_readlane((int)sp.w, l));
+        const uint4 sl = make_uint4((uint32_t)__builtin_amdgcn_readfirstlane((int)stage[5 * l]),
+                                    (uint32_t)__builtin_amdgcn_readfirstlane((int)stage[5 * l + 1]),
+                                    (uint32_t)__builtin_amdgcn_readfirstlane((int)stage[5 * l + 2]),
+                                    (uint32_t)__builtin_amdgcn_readfirstlane((int)stage[5 * l + 3]));
+        const bool kp = __builtin_amdgcn_readfirstlane((int)stage[5 * l + 4]) != 0;
         const Scal sv = unpack(sl);
         if (a.tinfo) coop_write_info(st, g, el, sv, a.tinfo + el * PE_NINFO, lane);
-        const bool kp = __builtin_amdgcn_readlane((int)keep, l) != 0;
         Row4<MAXW> rw;
         const Scal ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane);
         asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
         coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
-        if (lane == l) s = ns;
-      }
-      if (done) {
-        st.ep_ret[e] = 0.0;
-        st.scal[e] = pack(s);
+        const uint4 np = pack(ns);
+        if (lane == 0) {
+          stage[5 * l] = np.x;
+          stage[5 * l + 1] = np.y;
+          stage[5 * l + 2] = np.z;
+          stage[5 * l + 3] = np.w;
+        }
       }
     }
-    __syncthreads();  // fresh tile rows complete before the tile store
+    __syncthreads();  // fresh tile rows and new scalars complete
+    if (wv == CW && done) {
+      s = unpack(make_uint4(stage[5 * lane], stage[5 * lane + 1], stage[5 * lane + 2], stage[5 * lane + 3]));
+      st.ep_ret[e] = 0.0;
+      st.scal[e] = pack(s);
+    }
     return pack(s);
   }
   // Many done envs (a synchronized batch truncating together): one lane per env.
@@ -669,7 +697,7 @@ __device__ __forceinline__ void quad_done_obs(const void* ka, int tile_off, int 
 }
 
 template <int C, int R, bool ONEWORD, int NW>
-__global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs
   constexpr int NR = 2 * R + 3, NV = 7, EPB = kQuadEnvs, CW = NW - 1;  // CW: commit wave
   static_assert(C % NW == 0, "rays must split evenly over the waves");
   static_assert(ONEWORD || R <= 14, "funnel-shifted window row must hold 2R+5 cells");
@@ -950,12 +978,20 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   }
   PE_STAMP(4);
   // ---- DummyVecEnv auto-reset (rare): commit wave, after the whole obs row is in LDS
-  const int ndone = __syncthreads_count(done);  // done envs of the block (0: the usual case)
-  const bool any_done = ndone > 0;
+  // any env of the block done (the usual answer: no)?  The commit wave's done mask
+  // goes to an unused LDS table word (dist[70..71]) for the count the reset path needs.
+  static_assert(R < 70, "dist[70..71] holds the done mask");
+  if (wv == CW) {
+    const uint64_t dm = __ballot(done);
+    if (lane == 0) reinterpret_cast<uint64_t*>(smem)[35] = dm;
+  }
+  const bool any_done = __syncthreads_or(done);
+  const int ndone = any_done ? __popcll(reinterpret_cast<const uint64_t*>(smem)[35]) : 0;
   PE_STAMP(5);
   // auto-reset slow path, out of line (its registers stay off the hot path)
   static_assert(2 * C * R <= (NR * 8 + NV * 4) * EPB, "LIDAR offset tables must fit the window region");
-  if (any_done) {
+  static_assert(5 * 4 * EPB + 8 <= (NR * 8 + NV * 4) * EPB, "reset staging must fit the window region");
+  if (__builtin_expect(any_done, 0)) {  // cold: laid out after the hot path
     const uint4 ns = quad_done_path<NW, ONEWORD>(kernargs(), quad_tile_off<R>(), C, R, lane, wv, CW, e0, done,
                                                  pack(s), ret, ndone);
     s = unpack(ns);
@@ -1271,6 +1307,7 @@ StepArgs base_args(const pe_handle* h) {
   a.n = h->n;
   a.autoreset = h->cfg.autoreset;
   a.stagger = h->stagger;
+  a.coop_max_done = h->coop_max_done;
   return a;
 }
 
@@ -1470,12 +1507,12 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   // grid image in HBM (no room for it in the obs-tile row), where it is ~30x
   // slower (29 ms for a whole 64x64 batch) and the cooperative path always wins.
   if (!coop_reset_ok(G, g.WPR, g.NW, P, C, c->map_generation_algo))
-    rl.coop_max_done = 0;
+    h->coop_max_done = 0;
   else if (reset_scratch_bytes(G, g.WPR, P) <= 4 * g.D)
-    rl.coop_max_done = kCoopMaxDone;
+    h->coop_max_done = kCoopMaxDone;
   else
-    rl.coop_max_done = kQuadEnvs;
-  if (const char* cm = std::getenv("PE_COOP_MAX_DONE")) rl.coop_max_done = std::atoi(cm);  // A/B
+    h->coop_max_done = kQuadEnvs;
+  if (const char* cm = std::getenv("PE_COOP_MAX_DONE")) h->coop_max_done = std::atoi(cm);  // A/B
   rl.max_steps = c->max_steps;
 
   // host tables

@@ -20,10 +20,12 @@ for w in $WHAT; do
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/tests_$TAG.log 2>&1 ;;
     bench)
       timeout -k 10 300 python bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err ;;
+    benchd)
+      timeout -k 10 300 python bench.py --desync --steps 20000 --warmup 200 --no-cpu-baseline > $OUT/benchd_$TAG.json 2> $OUT/benchd_$TAG.err ;;
     benchq)
       timeout -k 10 300 python bench.py --steps 4000 --warmup 200 --no-cpu-baseline > $OUT/benchq_$TAG.json 2> $OUT/benchq_$TAG.err ;;
     bench64)
-      timeout -k 10 300 python bench.py --grid 64 --rays 64 --range 6 --steps 500 --warmup 50 \
+      timeout -k 10 300 python bench.py --grid 64 --rays 64 --range 6 --steps 3000 --warmup 100 \
         --cpu-seconds 5 > $OUT/bench64_$TAG.json 2> $OUT/bench64_$TAG.err ;;
     stats)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/stats_$TAG -o run -- \
