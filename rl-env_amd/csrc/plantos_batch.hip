@@ -1012,6 +1012,41 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
   PE_STAMP(7);
 }
 
+// reset() with one wave per env (pe_coop.hpp): the map, grid/visit rows and the
+// fresh obs of env e by the 64 lanes of wave e % 4 of block e / 4 -- 65536 envs
+// are 65536 waves, so the whole chip generates maps at once (the lane-per-env
+// kernel below gives one env per lane: 29 ms at 64x64, where it scans its grid
+// image in HBM).  Unmasked envs rebuild their obs from the current state.
+template <int MAXW>
+__global__ __launch_bounds__(256) void pe_reset_coop_kernel(StepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const Geo& g = a.g;
+  load_tables(smem, a.st.tab);
+  __syncthreads();
+  const float* tdist = smem;
+  const float* tpos = smem + 72;
+  const float* tvis = smem + 328;
+  const int lane = threadIdx.x & 63;
+  const int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (e >= a.n) return;  // wave-uniform
+  const Scal s = unpack(a.st.scal[e]);
+  const bool resetting = !a.mask || a.mask[e];
+  if (resetting) {
+    bool keep = false;
+    if (a.st.cur && lane == 0) keep = curriculum_on_reset(a.st.cur, e, a.rl);  // A2C_training.py:56-95
+    keep = __builtin_amdgcn_readfirstlane((int)keep) != 0;
+    Row4<MAXW> rw;
+    const Scal ns = coop_reset_env<MAXW>(a.st, g, a.rl, e, s.episode, keep, rw, lane);
+    if (lane == 0) {
+      a.st.ep_ret[e] = 0.0;
+      a.st.scal[e] = pack(ns);
+    }
+    if (a.obs) coop_fresh_obs<MAXW>(g, rw, ns, a.obs + e * g.D, tdist, tpos, tvis, a.st.ldx, a.st.ldy, lane);
+  } else if (a.obs && lane == 0) {
+    build_obs_generic(a, e, s.x, s.y, a.obs + e * g.D, tdist, tpos, tvis, a.st.ldx, a.st.ldy);
+  }
+}
+
 // reset(): masked device-rng reset, then obs of every env (obs may be NULL).
 __global__ __launch_bounds__(kBlock) void pe_reset_kernel(StepArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1362,6 +1397,16 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
 }
 
 int launch_reset(const pe_handle* h, const StepArgs& a, hipStream_t s) {
+  if (h->coop_max_done > 0) {  // the cooperative reset applies (pe_coop.hpp coop_reset_ok)
+    dim3 cgrid((unsigned)((h->n + 3) / 4)), cblock(256);
+    const size_t clds = sizeof(float) * (size_t)kTabFloats;
+    if (h->g.WPR == 1)
+      hipLaunchKernelGGL(pe_reset_coop_kernel<1>, cgrid, cblock, clds, s, a);
+    else
+      hipLaunchKernelGGL(pe_reset_coop_kernel<kCoopWPR>, cgrid, cblock, clds, s, a);
+    PE_HIP(hipGetLastError());
+    return PE_OK;
+  }
   dim3 grid((unsigned)((h->n + kBlock - 1) / kBlock)), block(kBlock);
   size_t lds = lds_bytes(h->g);
   hipLaunchKernelGGL(pe_reset_kernel, grid, block, lds, s, a);
