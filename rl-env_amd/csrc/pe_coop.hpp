@@ -28,6 +28,20 @@
 
 namespace pe {
 
+#ifdef PE_COOP_TIMING  // tools/diag/coop_bench.hip only: phase cycle stamps of block 0
+__device__ unsigned long long g_coop_t[8];
+#define PE_COOP_T(k)                                                     \
+  do {                                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                   \
+    const unsigned long long _t = __builtin_readcyclecounter();          \
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_coop_t[k] += _t;          \
+  } while (0)
+#else
+#define PE_COOP_T(k) \
+  do {               \
+  } while (0)
+#endif
+
 constexpr int kCoopWPR = 4;     // row words per lane: G + 2R <= 128
 constexpr int kCoopMaxDone = 8; // done envs per block up to which the cooperative path is taken
 
@@ -129,6 +143,19 @@ struct WaveStream {
     c3 = t[3];
     pos = 0;
   }
+  // restart the batch at the block holding word `pos`: words pos .. pos+252 available
+  __device__ __forceinline__ void realign(int lane) {
+    const uint32_t a = base * 4u + (uint32_t)pos;  // absolute word index
+    base = a >> 2;
+    fill(lane);
+    pos = (int)(a & 3u);
+  }
+  // word q (< 256) of the batch, for each lane its own q
+  __device__ __forceinline__ uint32_t word_at(int q) const {
+    const int src = q & 63;
+    return pick4((uint32_t)__shfl((int)c0, src), (uint32_t)__shfl((int)c1, src), (uint32_t)__shfl((int)c2, src),
+                 (uint32_t)__shfl((int)c3, src), q >> 6);
+  }
   __device__ __forceinline__ void init(uint64_t seed, uint32_t env_id, uint32_t ep, int lane) {
     k0 = (uint32_t)seed;
     k1 = (uint32_t)(seed >> 32);
@@ -159,6 +186,20 @@ struct WaveStream {
     return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
   }
 };
+
+// per-lane position of the jj-th (0-based) set bit of m (jj < popcount(m))
+__device__ __forceinline__ int select_bit(uint64_t m, int jj) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const int low = __popcll(m & ((1ull << w) - 1ull));
+    const bool up = jj >= low;
+    jj -= up ? low : 0;
+    m = up ? (m >> w) : m;
+    pos += up ? w : 0;
+  }
+  return pos;
+}
 
 // code `code` at padded column pcol of this lane's row words
 template <int MAXW>
@@ -210,8 +251,10 @@ __device__ inline Scal coop_gen_map(const Geo& g, const Rules& rl, const Tables*
     real[w] = in ? tab->grid_real[w] : 0ull;
     rw.set(w, own && in ? tab->grid_pad[w] : 0ull);
   }
+  PE_COOP_T(0);
   WaveStream rng;
   rng.init(rl.seed, env_id, episode, lane);
+  PE_COOP_T(1);
   // obstacle clusters, plantos_env.py:341-354
   const int clusters = rl.O / 3;
   for (int q = 0; q < clusters; ++q) {
@@ -225,6 +268,7 @@ __device__ inline Scal coop_gen_map(const Geo& g, const Rules& rl, const Tables*
         if (0 <= oy && oy < G) coop_set(rw, oy + R, OBST);
       }
   }
+  PE_COOP_T(2);
   int c0 = 0, nob = 0;
 #pragma unroll
   for (int w = 0; w < MAXW; ++w) {
@@ -247,30 +291,97 @@ __device__ inline Scal coop_gen_map(const Geo& g, const Rules& rl, const Tables*
     s.expl = 0;
     return s;
   }
-  // random.sample(list(available), P): plants are not obstacles, so the kind-0
-  // counts stay valid for every pick; a pick of an already chosen cell redraws.
+  // random.sample(list(available), P) (:366), 64 draws per round.  The sequential
+  // form is: below(nfree) (words whose top k bits are >= nfree are skipped), map
+  // to the j-th non-obstacle cell, redraw if that cell is already chosen.  Plants
+  // are not obstacles, so the per-row counts stay valid for every pick; the
+  // accepted values are the stream's words in order, so 64 consecutive words are
+  // mapped to cells at once (row: binary search over the rows' prefix counts;
+  // column: per-lane bit select in the row word fetched from its owner lane), and
+  // the first (P - picked) of them whose cell is free and not hit by an earlier
+  // lane of the round become the next picks -- the sequential loop's result.
   // Pick i is kept in lane i % 64 (registers pk0 / pk1).
   const int i0 = wave_incl_scan(c0, lane), e0 = i0 - c0;
+  PE_COOP_T(3);
   int pk0 = 0, pk1 = 0;
-  for (int i = 0; i < rl.P; ++i) {
-    int row, pcol;
-    for (;;) {
-      coop_nth_cell(rw, g.WPR, real, i0, e0, (int)rng.below((uint32_t)nfree, lane), 0, lane, row, pcol);
-      const uint64_t word = readlane64(rw.get((2 * pcol) >> 6), row);
-      if (((word >> ((2 * pcol) & 63)) & 3u) == EMPTY) break;
-    }
-    if (lane == row) coop_set(rw, pcol, HYD);
-    const int cell = row * G + pcol - R;
-    if (lane == (i & 63)) {
-      if (i < 64) pk0 = cell;
-      else pk1 = cell;
+  {
+    const int kb = 32 - __clz((uint32_t)nfree);
+    int picked = 0;
+    while (picked < rl.P) {
+      if (rng.pos + 64 > 256) rng.realign(lane);
+      const uint32_t jv = rng.word_at(rng.pos + lane) >> (32 - kb);
+      const bool acc = jv < (uint32_t)nfree;
+      int row = 0;  // rows whose inclusive count is <= jv
+#pragma unroll
+      for (int st = 32; st >= 1; st >>= 1) {
+        const int probe = __shfl(i0, row + st - 1);
+        row += (uint32_t)probe <= jv ? st : 0;
+      }
+      row = acc ? row : 0;
+      int jj = (int)jv - __shfl(e0, row);
+      Row4<MAXW> rv{0ull, 0ull, 0ull, 0ull};
+#pragma unroll
+      for (int w = 0; w < MAXW; ++w)
+        if (MAXW == 1 || w < g.WPR) rv.set(w, shfl64(rw.get(w), row));
+      int col = 0;
+#pragma unroll
+      for (int w = 0; w < MAXW; ++w) {
+        if (MAXW == 1 || w < g.WPR) {
+          const uint64_t m = cand_mask(rv.get(w), real[w], 0);
+          const int c = __popcll(m);
+          if (jj >= 0 && jj < c) col = w * 32 + select_bit(m, jj) / 2;
+          jj -= c;
+        }
+      }
+      const bool valid = acc && ((rv.get((2 * col) >> 6) >> ((2 * col) & 63)) & 3u) == EMPTY;
+      const int cell = row * G + col - R;
+      bool dup = false;  // an earlier valid lane of this round chose the same cell
+      for (uint64_t um = __ballot(valid); um;) {
+        const int t = __ffsll((unsigned long long)um) - 1;
+        um &= um - 1;
+        dup = dup || (t < lane && __builtin_amdgcn_readlane(cell, t) == cell);
+      }
+      const bool surv = valid && !dup;
+      const uint64_t sm = __ballot(surv);
+      const int need = rl.P - picked, nsurv = __popcll(sm);
+      const int rank = __popcll(sm & ((1ull << lane) - 1ull));
+      const bool take = surv && rank < need;
+      // words consumed: through the last pick taken, else the whole round
+      rng.pos += nsurv >= need ? nth_set_bit(sm, need - 1, lane) + 1 : 64;
+      for (uint64_t tm = __ballot(take); tm;) {
+        const int t = __ffsll((unsigned long long)tm) - 1;
+        tm &= tm - 1;
+        const int rt = __builtin_amdgcn_readlane(row, t), ct = __builtin_amdgcn_readlane(col, t);
+        const int idx = picked + __builtin_amdgcn_readlane(rank, t);
+        const int cellt = __builtin_amdgcn_readlane(cell, t);
+        if (lane == rt) coop_set(rw, ct, HYD);
+        if (lane == (idx & 63)) {
+          if (idx < 64) pk0 = cellt;
+          else pk1 = cellt;
+        }
+      }
+      picked += nsurv < need ? nsurv : need;
     }
   }
-  // thirsty draws in sample order, plantos_env.py:367-369
-  for (int i = 0; i < rl.P; ++i) {
-    const int c = __builtin_amdgcn_readlane(i < 64 ? pk0 : pk1, i & 63);
-    if (rng.random53(lane) < rl.p_thirsty && lane == c / G) coop_set(rw, c % G + R, THIRSTY);
+  PE_COOP_T(4);
+  // thirsty draws in sample order, plantos_env.py:367-369: random() = 2 words
+  // each, no rejection -- pick i draws words 2i, 2i+1 after the sample
+  for (int base_i = 0; base_i < rl.P; base_i += 64) {
+    const int cnt = rl.P - base_i < 64 ? rl.P - base_i : 64;
+    if (rng.pos + 2 * cnt > 256) rng.realign(lane);
+    const uint32_t a = rng.word_at(rng.pos + 2 * lane) >> 5, b = rng.word_at(rng.pos + 2 * lane + 1) >> 6;
+    const double r = ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
+    const bool th = lane < cnt && r < rl.p_thirsty;
+    const int cell = base_i == 0 ? pk0 : pk1;
+    rng.pos += 2 * cnt;
+    for (uint64_t tm = __ballot(th); tm;) {
+      const int t = __ffsll((unsigned long long)tm) - 1;
+      tm &= tm - 1;
+      const int c = __builtin_amdgcn_readlane(cell, t);
+      if (lane == c / G) coop_set(rw, c % G + R, THIRSTY);
+    }
   }
+  PE_COOP_T(5);
   // rover: choice(list(available - plants)), plantos_env.py:370-372
   int c1 = 0;
 #pragma unroll
@@ -280,6 +391,7 @@ __device__ inline Scal coop_gen_map(const Geo& g, const Rules& rl, const Tables*
   coop_nth_cell(rw, g.WPR, real, i1, i1 - c1, (int)rng.below((uint32_t)(nfree - rl.P), lane), 1, lane, row, pcol);
   s.x = row;
   s.y = pcol - R;
+  PE_COOP_T(6);
   return s;
 }
 

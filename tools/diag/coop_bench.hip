@@ -2,6 +2,7 @@
 // env on one wave (256 workgroups of one wave, each resetting K envs in a row).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o build/coop_bench tools/diag/coop_bench.hip
 #include <hip/hip_runtime.h>
+#define PE_COOP_TIMING 1
 #include <cstdio>
 #include <cstring>
 #include "../../rl-env_amd/csrc/pe_coop.hpp"
@@ -82,6 +83,12 @@ int main() {
     printf("\"%s_us_per_env\": %.2f, ", name, ms * 1000 / 5 / K);
   };
   run(k_coop<0>, "coop_gen_map");
+  {
+    unsigned long long t[8];
+    hipMemcpyFromSymbol(t, HIP_SYMBOL(g_coop_t), sizeof(t));
+    const char* nm[6] = {"init", "clusters", "count_scan", "sample", "thirsty", "rover"};
+    for (int k = 0; k < 6; ++k) printf("\"cyc_%s\": %.0f, ", nm[k], (double)(t[k + 1] - t[k]) / (7.0 * K));
+  }
   run(k_coop<1>, "rng_60_draws");
   run(k_coop<2>, "scans");
   run(k_coop<3>, "gen_plus_obs");
