@@ -29,6 +29,7 @@
 namespace pe {
 
 #ifdef PE_COOP_TIMING  // tools/diag/coop_bench.hip only: phase cycle stamps of block 0
+// (each stamp is a global read-modify-write: a few hundred cycles of its own)
 __device__ unsigned long long g_coop_t[8];
 #define PE_COOP_T(k)                                                     \
   do {                                                                   \
