@@ -48,8 +48,11 @@ constexpr int kCoopMaxDone = 8; // done envs per block up to which the cooperati
 
 // The cooperative path covers the original map generator with one grid row per
 // lane; everything else takes the lane-per-env path.
-__host__ __device__ constexpr bool coop_reset_ok(int G, int WPR, int NW, int P, int C, int map_algo) {
-  return G <= 64 && WPR <= kCoopWPR && NW <= kMaxNW && P <= 128 && C <= 64 && map_algo == 0;
+// The step kernel gives each of its 4 waves G x WPR words of LDS scratch after the
+// reset staging (1296 B) in the window-row region, (2R+3) x 512 + 7 x 256 B.
+__host__ __device__ constexpr bool coop_reset_ok(int G, int R, int WPR, int NW, int P, int C, int map_algo) {
+  return G <= 64 && WPR <= kCoopWPR && NW <= kMaxNW && P <= 128 && C <= 64 && map_algo == 0 &&
+         1296 + 4 * 8 * G * WPR <= (2 * R + 3) * 512 + 7 * 256;
 }
 
 __device__ __forceinline__ int wave_sum(int v) {
@@ -71,6 +74,10 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
   return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+__device__ __forceinline__ void lds_or64(uint64_t* p, uint64_t v) {
+  __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
@@ -240,9 +247,107 @@ __device__ __forceinline__ void coop_nth_cell(const Row4<MAXW>& rw, int WPR, con
 // Philox draws in the same order, rows in the lanes' registers.  Returns the new
 // scalars (uniform); rw holds the lane's grid row.  tab: the handle's tables in
 // global memory (uniform words: scalar loads).
+// The obstacle clusters of gen_map for G >= 5 (see coop_gen_map): OR-s the
+// cluster cells into scr (the caller merges); dbg (diagnostics, may be NULL)
+// receives cx, cy, size of each cluster.
+__device__ inline void coop_clusters(const Geo& g, int clusters, WaveStream& rng, uint64_t* scr, int lane,
+                                     int* dbg) {
+  const int G = g.G, R = g.R;
+  const int k1 = 32 - __clz((uint32_t)(G - 4));
+  int state = 0, emitted = 0;  // uniform: draw state at the round start, values emitted
+  int carry1 = 0, carry2 = 0;  // the last two values emitted before this round (cy, cx)
+  while (emitted < 3 * clusters) {
+    if (rng.pos + 64 > 256) rng.realign(lane);
+    const uint32_t wd = rng.word_at(rng.pos + lane);
+    const bool a1 = (wd >> (32 - k1)) < (uint32_t)(G - 4), a2 = (wd >> 30) < 2u;
+    // map: s -> next state; 2 bits per state
+    int f = (a1 ? 1 : 0) | ((a1 ? 2 : 1) << 2) | ((a2 ? 0 : 2) << 4);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {  // F(lane) = f(lane) o F(lane - 1)
+      const int t = __shfl_up(f, o);
+      if (lane >= o)
+        f = ((f >> (2 * (t & 3))) & 3) | (((f >> (2 * ((t >> 2) & 3))) & 3) << 2) |
+            (((f >> (2 * ((t >> 4) & 3))) & 3) << 4);
+    }
+    // (the shuffle outside the select: inside `lane == 0 ? ... : __shfl_up()` it is
+    // evaluated with lane 0 inactive, and lane 1 then reads an inactive lane)
+    const int fup = __shfl_up(f, 1);
+    const int fprev = lane == 0 ? (0 | (1 << 2) | (2 << 4)) : fup;
+    const int st = (fprev >> (2 * state)) & 3;  // draw state before this word
+    const bool emit = st < 2 ? a1 : a2;
+    const int val = 2 + (int)(st < 2 ? (wd >> (32 - k1)) : (wd >> 30));
+    const uint64_t em = __ballot(emit);
+    const int rank = emitted + __popcll(em & ((1ull << lane) - 1ull));
+    const bool use = emit && rank < 3 * clusters;
+    // the two emitting lanes before this one (or the carried values)
+    const uint64_t before = em & ((1ull << lane) - 1ull);
+    const int p1 = before ? 63 - __clzll((long long)before) : -1;
+    const uint64_t before2 = p1 >= 0 ? (before & ~(1ull << p1)) : 0ull;
+    const int p2 = before2 ? 63 - __clzll((long long)before2) : -1;
+    const int v1 = __shfl(val, p1 < 0 ? 0 : p1), v2 = __shfl(val, p2 < 0 ? 0 : p2);
+    if (use && st == 2) {  // this lane completes a cluster
+      const int cy = p1 >= 0 ? v1 : carry1;
+      const int cx = p2 >= 0 ? v2 : (p1 >= 0 ? carry1 : carry2);
+      const int size = val;
+      if (dbg) {
+        dbg[3 * (rank / 3)] = cx;
+        dbg[3 * (rank / 3) + 1] = cy;
+        dbg[3 * (rank / 3) + 2] = size;
+      }
+      for (int dx = 0; dx < size; ++dx) {
+        const int ox = cx + dx - size / 2;
+        if (ox < 0 || ox >= G) continue;
+        for (int dy = 0; dy < size; ++dy) {
+          const int oy = cy + dy - size / 2;
+          if (0 <= oy && oy < G) {
+            const int bit = 2 * (oy + R);
+            lds_or64(scr + ox * g.WPR + (bit >> 6), 1ull << (bit & 63));  // code OBST
+          }
+        }
+      }
+    }
+    const int nem = __popcll(em), take = 3 * clusters - emitted;
+    if (nem >= take) {  // the last cluster's size: consume through that word
+      rng.pos += nth_set_bit(em, take - 1, lane) + 1;
+      emitted += take;
+    } else {
+      // carry the last two emitted values (by rank) into the next round
+      if (nem >= 2) {
+        const int l1 = 63 - __clzll((long long)em), l2 = 63 - __clzll((long long)(em & ~(1ull << l1)));
+        carry1 = __shfl(val, l1);
+        carry2 = __shfl(val, l2);
+      } else if (nem == 1) {
+        carry2 = carry1;
+        carry1 = __shfl(val, 63 - __clzll((long long)em));
+      }
+      state = (__builtin_amdgcn_readlane(f, 63) >> (2 * state)) & 3;  // through all 64 words
+      rng.pos += 64;
+      emitted += nem;
+    }
+  }
+}
+
+// LDS scratch of one wave for the cooperative reset: G rows x WPR words (the
+// obstacle / plant bits of a round, OR-ed in by the lanes that drew them).
+__host__ __device__ constexpr int coop_scratch_words(int G, int WPR) { return G * WPR; }
+
+// OR the round's bits (scr, G x WPR words, written with LDS atomics) into each
+// lane's row, and clear them for the next round.
+template <int MAXW>
+__device__ __forceinline__ void coop_merge(Row4<MAXW>& rw, uint64_t* scr, int WPR, int G, int lane) {
+  if (lane < G) {
+#pragma unroll
+    for (int w = 0; w < MAXW; ++w)
+      if (MAXW == 1 || w < WPR) {
+        rw.set(w, rw.get(w) | scr[lane * WPR + w]);
+        scr[lane * WPR + w] = 0ull;
+      }
+  }
+}
+
 template <int MAXW>
 __device__ inline Scal coop_gen_map(const Geo& g, const Rules& rl, const Tables* tab, Row4<MAXW>& rw,
-                                    uint32_t env_id, uint32_t episode, int lane) {
+                                    uint32_t env_id, uint32_t episode, int lane, uint64_t* scr) {
   const int G = g.G, R = g.R;
   const bool own = lane < G;
   uint64_t real[MAXW];
@@ -256,18 +361,31 @@ __device__ inline Scal coop_gen_map(const Geo& g, const Rules& rl, const Tables*
   WaveStream rng;
   rng.init(rl.seed, env_id, episode, lane);
   PE_COOP_T(1);
-  // obstacle clusters, plantos_env.py:341-354
+  if (own)
+    for (int w = 0; w < g.WPR; ++w) scr[lane * g.WPR + w] = 0ull;
+  // obstacle clusters, plantos_env.py:341-354: cx = 2 + below(G-4), cy = 2 +
+  // below(G-4), size = 2 + below(2) per cluster.  64 words per round: which draw
+  // a word serves depends on the words before it (rejections), so each word's
+  // effect on the draw state {cx, cy, size} is a 3-state map, and an inclusive
+  // scan of map compositions gives every lane its state; the accepting lanes
+  // emit the values, each size-lane assembles its cluster from the two emitting
+  // lanes before it (or the previous round's carry) and ORs its obstacle bits in.
   const int clusters = rl.O / 3;
-  for (int q = 0; q < clusters; ++q) {
-    const int cx = 2 + (int)rng.below((uint32_t)(G - 4), lane);
-    const int cy = 2 + (int)rng.below((uint32_t)(G - 4), lane);
-    const int size = 2 + (int)rng.below(2u, lane);
-    const int x0 = cx - size / 2;
-    if (own && lane >= x0 && lane < x0 + size)
-      for (int dy = 0; dy < size; ++dy) {
-        const int oy = cy + dy - size / 2;
-        if (0 <= oy && oy < G) coop_set(rw, oy + R, OBST);
-      }
+  if (G - 4 >= 1) {
+    coop_clusters(g, clusters, rng, scr, lane, nullptr);
+    coop_merge(rw, scr, g.WPR, G, lane);
+  } else {  // G <= 4: below(0) draws nothing; the plain sequential form
+    for (int q = 0; q < clusters; ++q) {
+      const int cx = 2 + (int)rng.below((uint32_t)(G - 4), lane);
+      const int cy = 2 + (int)rng.below((uint32_t)(G - 4), lane);
+      const int size = 2 + (int)rng.below(2u, lane);
+      const int x0 = cx - size / 2;
+      if (own && lane >= x0 && lane < x0 + size)
+        for (int dy = 0; dy < size; ++dy) {
+          const int oy = cy + dy - size / 2;
+          if (0 <= oy && oy < G) coop_set(rw, oy + R, OBST);
+        }
+    }
   }
   PE_COOP_T(2);
   int c0 = 0, nob = 0;
@@ -349,19 +467,20 @@ __device__ inline Scal coop_gen_map(const Geo& g, const Rules& rl, const Tables*
       const bool take = surv && rank < need;
       // words consumed: through the last pick taken, else the whole round
       rng.pos += nsurv >= need ? nth_set_bit(sm, need - 1, lane) + 1 : 64;
-      for (uint64_t tm = __ballot(take); tm;) {
-        const int t = __ffsll((unsigned long long)tm) - 1;
-        tm &= tm - 1;
-        const int rt = __builtin_amdgcn_readlane(row, t), ct = __builtin_amdgcn_readlane(col, t);
-        const int idx = picked + __builtin_amdgcn_readlane(rank, t);
-        const int cellt = __builtin_amdgcn_readlane(cell, t);
-        if (lane == rt) coop_set(rw, ct, HYD);
-        if (lane == (idx & 63)) {
-          if (idx < 64) pk0 = cellt;
-          else pk1 = cellt;
-        }
+      // the picks of the round: plant bits into the owner rows (LDS atomics); lane L
+      // keeps pick L (pk0) / L + 64 (pk1), pulled from the lane that took it (the
+      // rho-th survivor, rho = its rank in the round)
+      if (take) {
+        const int bit = 2 * col;
+        lds_or64(scr + row * g.WPR + (bit >> 6), (uint64_t)HYD << (bit & 63));
       }
-      picked += nsurv < need ? nsurv : need;
+      const int ntake = nsurv < need ? nsurv : need;
+      const int rho = (lane - picked) & 63;
+      const int got = __shfl(cell, rho < ntake ? select_bit(sm, rho) : 0);
+      pk0 = lane >= picked && lane < picked + ntake ? got : pk0;
+      pk1 = lane + 64 >= picked && lane + 64 < picked + ntake ? got : pk1;
+      coop_merge(rw, scr, g.WPR, G, lane);
+      picked += ntake;
     }
   }
   PE_COOP_T(4);
@@ -375,12 +494,11 @@ __device__ inline Scal coop_gen_map(const Geo& g, const Rules& rl, const Tables*
     const bool th = lane < cnt && r < rl.p_thirsty;
     const int cell = base_i == 0 ? pk0 : pk1;
     rng.pos += 2 * cnt;
-    for (uint64_t tm = __ballot(th); tm;) {
-      const int t = __ffsll((unsigned long long)tm) - 1;
-      tm &= tm - 1;
-      const int c = __builtin_amdgcn_readlane(cell, t);
-      if (lane == c / G) coop_set(rw, c % G + R, THIRSTY);
+    if (th) {  // hydrated (2) -> thirsty (3): the low bit of the plant's code
+      const int bit = 2 * (cell % G + R);
+      lds_or64(scr + (cell / G) * g.WPR + (bit >> 6), 1ull << (bit & 63));
     }
+    coop_merge(rw, scr, g.WPR, G, lane);
   }
   PE_COOP_T(5);
   // rover: choice(list(available - plants)), plantos_env.py:370-372
@@ -434,9 +552,9 @@ __device__ inline void coop_write_info(const State& st, const Geo& g, int64_t e,
 // new_episode_visits.  keep: CurriculumWrapper keeps the previous visit counts.
 template <int MAXW>
 __device__ inline Scal coop_reset_env(const State& st, const Geo& g, const Rules& rl, int64_t e, uint32_t episode,
-                                      bool keep, Row4<MAXW>& rw, int lane) {
+                                      bool keep, Row4<MAXW>& rw, int lane, uint64_t* scr) {
   const Tables* tab = st.tab;
-  Scal s = coop_gen_map<MAXW>(g, rl, tab, rw, rl.env_off + (uint32_t)e, episode, lane);
+  Scal s = coop_gen_map<MAXW>(g, rl, tab, rw, rl.env_off + (uint32_t)e, episode, lane, scr);
   if ((s.flags & F_NOROOM) && lane == 0) atomicOr(st.err_bits, F_NOROOM);
   if (lane < g.G) {
     uint64_t* gb = st.grid + e * g.gstride + (int64_t)lane * g.WPR;

@@ -617,7 +617,8 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         const Scal sv = unpack(sl);
         if (a.tinfo) coop_write_info(st, g, el, sv, a.tinfo + el * PE_NINFO, lane);
         Row4<MAXW> rw;
-        const Scal ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane);
+        uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
+        const Scal ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane, scr);
         asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
         coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
         const uint4 np = pack(ns);
@@ -1036,7 +1037,8 @@ __global__ __launch_bounds__(256) void pe_reset_coop_kernel(StepArgs a) {
     if (a.st.cur && lane == 0) keep = curriculum_on_reset(a.st.cur, e, a.rl);  // A2C_training.py:56-95
     keep = __builtin_amdgcn_readfirstlane((int)keep) != 0;
     Row4<MAXW> rw;
-    const Scal ns = coop_reset_env<MAXW>(a.st, g, a.rl, e, s.episode, keep, rw, lane);
+    uint64_t* scr = reinterpret_cast<uint64_t*>(smem + kTabFloats) + (threadIdx.x >> 6) * coop_scratch_words(g.G, g.WPR);
+    const Scal ns = coop_reset_env<MAXW>(a.st, g, a.rl, e, s.episode, keep, rw, lane, scr);
     if (lane == 0) {
       a.st.ep_ret[e] = 0.0;
       a.st.scal[e] = pack(ns);
@@ -1399,7 +1401,7 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
 int launch_reset(const pe_handle* h, const StepArgs& a, hipStream_t s) {
   if (h->coop_max_done > 0) {  // the cooperative reset applies (pe_coop.hpp coop_reset_ok)
     dim3 cgrid((unsigned)((h->n + 3) / 4)), cblock(256);
-    const size_t clds = sizeof(float) * (size_t)kTabFloats;
+    const size_t clds = sizeof(float) * (size_t)kTabFloats + 4 * 8 * (size_t)coop_scratch_words(h->g.G, h->g.WPR);
     if (h->g.WPR == 1)
       hipLaunchKernelGGL(pe_reset_coop_kernel<1>, cgrid, cblock, clds, s, a);
     else
@@ -1551,7 +1553,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   // when many are done together -- unless the lane path would have to scan its
   // grid image in HBM (no room for it in the obs-tile row), where it is ~30x
   // slower (29 ms for a whole 64x64 batch) and the cooperative path always wins.
-  if (!coop_reset_ok(G, g.WPR, g.NW, P, C, c->map_generation_algo))
+  if (!coop_reset_ok(G, R, g.WPR, g.NW, P, C, c->map_generation_algo))
     h->coop_max_done = 0;
   else if (reset_scratch_bytes(G, g.WPR, P) <= 4 * g.D)
     h->coop_max_done = kCoopMaxDone;

@@ -14,6 +14,7 @@ template <int MODE>
 __global__ __launch_bounds__(64) void k_coop(Geo g, Rules rl, const Tables* tab, uint32_t* out) {
   __shared__ Tables lt;
   __shared__ float row[400];
+  __shared__ uint64_t scr[64 * 4];
   __shared__ signed char ldx[96], ldy[96];
   if (threadIdx.x == 0) lt = *tab;
   for (int k = threadIdx.x; k < 96; k += 64) {
@@ -27,7 +28,7 @@ __global__ __launch_bounds__(64) void k_coop(Geo g, Rules rl, const Tables* tab,
     const uint32_t env = blockIdx.x * K + i;
     if (MODE == 0) {  // coop_gen_map
       Row4<1> rw;
-      Scal s = coop_gen_map<1>(g, rl, &lt, rw, env, 0, lane);
+      Scal s = coop_gen_map<1>(g, rl, &lt, rw, env, 0, lane, scr);
       acc += s.x * 31 + s.y + (uint32_t)rw.w0;
     } else if (MODE == 1) {  // the rng draws alone (uniform)
       WaveStream r;
@@ -48,7 +49,7 @@ __global__ __launch_bounds__(64) void k_coop(Geo g, Rules rl, const Tables* tab,
       if (lane == 0 && i == K - 1) out[256 * 64 + blockIdx.x] = (uint32_t)(__builtin_readcyclecounter() - t0);
     } else if (MODE == 3) {  // gen + fresh obs
       Row4<1> rw;
-      Scal s = coop_gen_map<1>(g, rl, &lt, rw, env, 0, lane);
+      Scal s = coop_gen_map<1>(g, rl, &lt, rw, env, 0, lane, scr);
       coop_fresh_obs(g, rw, s, row, lt.dist, lt.pos, lt.vis, ldx, ldy, lane);
       acc += __float_as_uint(row[lane]);
     }
