@@ -44,7 +44,8 @@ __device__ unsigned long long g_coop_t[8];
 #endif
 
 constexpr int kCoopWPR = 4;     // row words per lane: G + 2R <= 128
-constexpr int kCoopMaxDone = 8; // done envs per block up to which the cooperative path is taken
+constexpr int kCoopMaxDone = 8;  // done envs per block up to which the cooperative path is taken
+constexpr int kPrefetchEvery = 64;  // steps between prefetch launches (queue mode)
 
 // The cooperative path covers the original map generator with one grid row per
 // lane; everything else takes the lane-per-env path.
@@ -515,8 +516,9 @@ __device__ inline Scal coop_gen_map(const Geo& g, const Rules& rl, const Tables*
 }
 
 // _get_info (plantos_env.py:317-336) of env e's current state by one wave
-// (write_info's columns); s: the env's scalars (uniform).
-__device__ inline void coop_write_info(const State& st, const Geo& g, int64_t e, const Scal& s, int32_t* o, int lane) {
+// (write_info's columns); s: the env's scalars (uniform); wfix: see write_info.
+__device__ inline void coop_write_info(const State& st, const Geo& g, int64_t e, const Scal& s, int32_t* o, int lane,
+                                       int wfix = 0) {
   int th = 0, hy = 0;
   if (lane < g.G)
     for (int w = 0; w < g.WPR; ++w) {
@@ -527,8 +529,8 @@ __device__ inline void coop_write_info(const State& st, const Geo& g, int64_t e,
       th += __popcll(lo & hi & real);   // sum(plants.values())     :318
       hy += __popcll(~lo & hi & real);  // len(plants) - thirsty    :319
     }
-  th = wave_sum(th);
-  hy = wave_sum(hy);
+  th = wave_sum(th) - wfix;
+  hy = wave_sum(hy) + wfix;
   int v = 0;
   switch (lane) {
     case 0: v = s.x; break;                             // rover_position     :324
@@ -547,14 +549,75 @@ __device__ inline void coop_write_info(const State& st, const Geo& g, int64_t e,
   if (lane < PE_NINFO) o[lane] = v;
 }
 
-// reset() of env e (plantos_env.py:125-158) by one wave: map, grid rows and visit
-// rows to HBM (lane r writes row r), the curriculum's carried-visits mode as
-// new_episode_visits.  keep: CurriculumWrapper keeps the previous visit counts.
+// Prefetched resets: the map of an env's NEXT reset depends only on (seed, env,
+// episode counter) -- never on how the current episode goes -- so it is generated
+// ahead of time, in batches, by pe_prefetch_kernel (one wave per env, thousands of
+// envs per launch: throughput, not latency), and the step kernel's auto-reset
+// copies it in (one memory round trip) instead of generating it on the critical
+// path of its block.  A record is valid for the reset whose episode counter is
+// scal.w - 1 (coop_gen_map returns episode + 1); scal.w == 0: no record
+// (struct Prefetch, pe_device.hpp).
+
+// Env e's prefetched reset record, loaded (PfLoad) before the caller's other
+// memory round trips (terminal info) and taken (coop_take_prefetched) after them:
+// if the record holds the reset of episode counter `episode`, its scalars go to s,
+// its rows to rw and its fresh obs row (D <= 64 * KD floats) to out.  Short rows
+// come in with the record (one round trip); longer ones after the check
+// (registers).
+template <int MAXW, int KD>
+struct PfLoad {
+  static constexpr bool kEarly = KD <= 2;
+  uint4 ps;
+  Row4<MAXW> rw;
+  float ov[kEarly ? KD : 1];
+};
+
+template <int MAXW, int KD>
+__device__ __forceinline__ void coop_load_prefetched(const Prefetch& pf, const Geo& g, int64_t e,
+                                                     PfLoad<MAXW, KD>& L, int lane) {
+  L.ps = pf.scal[e];
+  L.rw = Row4<MAXW>{0ull, 0ull, 0ull, 0ull};
+  if (lane < g.G) {
+    const uint64_t* src = pf.grid + e * g.gstride + (int64_t)lane * g.WPR;
+#pragma unroll
+    for (int w = 0; w < MAXW; ++w)
+      if (MAXW == 1 || w < g.WPR) L.rw.set(w, src[w]);
+  }
+  if constexpr (PfLoad<MAXW, KD>::kEarly) {
+    const float* osrc = pf.obs + e * g.D;
+#pragma unroll
+    for (int j = 0; j < KD; ++j) L.ov[j] = lane + 64 * j < g.D ? osrc[lane + 64 * j] : 0.0f;
+  }
+}
+
+template <int MAXW, int KD>
+__device__ __forceinline__ bool coop_take_prefetched(const Prefetch& pf, const Geo& g, int64_t e, uint32_t episode,
+                                                     const PfLoad<MAXW, KD>& L, Row4<MAXW>& rw, Scal& s, float* out,
+                                                     int lane) {
+  const uint32_t key = (uint32_t)__builtin_amdgcn_readfirstlane((int)L.ps.w);
+  if (key != episode + 1u) return false;
+  s = unpack(make_uint4((uint32_t)__builtin_amdgcn_readfirstlane((int)L.ps.x),
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)L.ps.y),
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)L.ps.z), key));
+  rw = L.rw;
+  if constexpr (PfLoad<MAXW, KD>::kEarly) {
+#pragma unroll
+    for (int j = 0; j < KD; ++j)
+      if (lane + 64 * j < g.D) out[lane + 64 * j] = L.ov[j];
+  } else {
+    const float* osrc = pf.obs + e * g.D;
+    for (int k = lane; k < g.D; k += 64) out[k] = osrc[k];
+  }
+  return true;
+}
+
+// The state writes of reset() for env e by one wave, given its new map (rows in
+// the lanes' registers) and scalars s: grid rows and visit rows to HBM (lane r
+// writes row r), the curriculum's carried-visits mode as new_episode_visits.
+// keep: CurriculumWrapper keeps the previous visit counts.
 template <int MAXW>
-__device__ inline Scal coop_reset_env(const State& st, const Geo& g, const Rules& rl, int64_t e, uint32_t episode,
-                                      bool keep, Row4<MAXW>& rw, int lane, uint64_t* scr) {
-  const Tables* tab = st.tab;
-  Scal s = coop_gen_map<MAXW>(g, rl, tab, rw, rl.env_off + (uint32_t)e, episode, lane, scr);
+__device__ inline Scal coop_apply_reset(const State& st, const Geo& g, int64_t e, Scal s, bool keep,
+                                        const Row4<MAXW>& rw, int lane) {
   if ((s.flags & F_NOROOM) && lane == 0) atomicOr(st.err_bits, F_NOROOM);
   if (lane < g.G) {
     uint64_t* gb = st.grid + e * g.gstride + (int64_t)lane * g.WPR;
@@ -568,7 +631,7 @@ __device__ inline Scal coop_reset_env(const State& st, const Geo& g, const Rules
       const int bit = 4 * (s.y + 2);
       const bool rover = lane == s.x && !(s.flags & F_NOROOM);
       for (int w = 0; w < g.NW; ++w) {
-        uint32_t v = tab->vis_pad[w];
+        uint32_t v = st.tab->vis_pad[w];
         if (rover && w == (bit >> 5)) v = (v & ~(0xFu << (bit & 31))) | (1u << (bit & 31));
         vb[w] = v;
       }
@@ -580,6 +643,15 @@ __device__ inline Scal coop_reset_env(const State& st, const Geo& g, const Rules
     s.flags |= F_EXPL_BITMAP;
   }
   return s;
+}
+
+// reset() of env e (plantos_env.py:125-158) by one wave: map generation, then
+// coop_apply_reset.
+template <int MAXW>
+__device__ inline Scal coop_reset_env(const State& st, const Geo& g, const Rules& rl, int64_t e, uint32_t episode,
+                                      bool keep, Row4<MAXW>& rw, int lane, uint64_t* scr) {
+  const Scal s = coop_gen_map<MAXW>(g, rl, st.tab, rw, rl.env_off + (uint32_t)e, episode, lane, scr);
+  return coop_apply_reset<MAXW>(st, g, e, s, keep, rw, lane);
 }
 
 // build_obs_fresh by one wave from the rows in the lanes' registers: lane i

@@ -93,6 +93,15 @@ struct State {
   CurRec* cur;             // batched CurriculumWrapper records, NULL when disabled
 };
 
+// Prefetched resets, see pe_coop.hpp coop_take_prefetched.
+struct Prefetch {
+  uint4* scal;      // [N] packed scalars the reset produces (before coop_apply_reset)
+  uint64_t* grid;   // [N][gstride] grid rows of the new map
+  float* obs;       // [N][D] fresh observation of the new episode
+  uint32_t* queue;  // [N] envs that consumed their record (the next batch to generate)
+  uint32_t* qn;     // [0] queued count, [1] ticket of the generating launch
+};
+
 struct Rules {
   double r_goal, r_mistake, r_invalid, r_water_empty, r_step, r_exploration, r_revisit, r_complete;
   double p_thirsty;
@@ -305,8 +314,10 @@ __device__ __forceinline__ bool expl_test_set(const State& st, const Geo& g, int
 
 // _get_info (plantos_env.py:317-336), integer columns (pe_info layout of
 // include/plantos_batch.h) for env e with scalars s.
+// wfix: the env's last watering (THIRSTY -> HYD) was not stored (an auto-reset
+// overwrites the grid rows, quad kernel commit).
 __device__ inline void write_info(const State& st, const Geo& g, const Tables* tab, int64_t e, const Scal& s,
-                                  int32_t* o) {
+                                  int32_t* o, int wfix = 0) {
   int th = 0, hy = 0;
   for (int row = 0; row < g.G; ++row)
     for (int w = 0; w < g.WPR; ++w) {
@@ -315,6 +326,8 @@ __device__ inline void write_info(const State& st, const Geo& g, const Tables* t
       th += __popcll(lo & hi & real);   // sum(plants.values())           :318
       hy += __popcll(~lo & hi & real);  // len(plants) - thirsty          :319
     }
+  th -= wfix;
+  hy += wfix;
   o[0] = s.x;                                 // rover_position           :324
   o[1] = s.y;
   o[2] = th;

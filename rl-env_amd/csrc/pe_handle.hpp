@@ -20,6 +20,11 @@ struct pe_handle {
   int quad_waves;    // waves per workgroup of the sector kernel (4 or 8; PE_QUAD_WAVES)
   int stagger;       // PE_STAGGER (experimental): sector-kernel start delay per block quarter
   int coop_max_done; // wave-cooperative auto-resets up to this many done envs per block (pe_coop.hpp)
+  pe::Prefetch pf;   // prefetched resets (pf.scal == NULL: off)
+  void* pf_mem;
+  int pf_every;      // steps between queue-mode prefetch launches (PE_PREFETCH_EVERY)
+  int pf_count;      // steps since the last one
+  int pf_blocks;     // queue-mode prefetch grid: workgroups resident at once
 };
 
 // pe_internal_set_error (plantos_batch.hip): records pe_last_error() for this thread.

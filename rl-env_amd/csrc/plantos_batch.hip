@@ -49,6 +49,7 @@ struct StepArgs {
   double* ep_ret_out;
   int32_t* ep_len_out;
   int32_t* tinfo;       // terminal _get_info rows of done envs (may be NULL)
+  Prefetch pf;          // prefetched resets (pe_coop.hpp); pf.scal == NULL: off
   int stagger;          // sector kernel: start delay per block quarter, units of 512 cycles
   const uint8_t* mask;  // reset kernel
 };
@@ -546,9 +547,9 @@ __device__ __forceinline__ bool quad_coop(const StepArgs& a, int ndone) {
 #endif
 }
 
-template <int NW, bool ONEWORD>  // one copy per kernel: each inherits its kernel's register budget
+template <int NW, bool ONEWORD, int KD>  // one copy per kernel: each inherits its kernel's register budget
 __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, int C, int R, int lane, int wv, int CW,
-                                                int64_t e0, bool done, uint4 sp, double ret, int ndone) {
+                                                int64_t e0, bool done, uint4 sp, double ret, int ndone, bool wfix) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const StepArgs& a = *reinterpret_cast<const StepArgs*>(ka);
   const Geo& g = a.g;
@@ -574,6 +575,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
     // its own lane, in program order.
     uint32_t* stage = reinterpret_cast<uint32_t*>(lrow);  // [64][5]: packed scalars, keep
     uint64_t* dmask = reinterpret_cast<uint64_t*>(stage + 5 * kQuadEnvs);
+    uint32_t* qbase = reinterpret_cast<uint32_t*>(dmask + 1);  // first prefetch-queue slot of the block
     const int NWv = blockDim.x >> 6;
     if (wv == CW) {
       bool keep = false;
@@ -585,13 +587,19 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         stage[5 * lane + 1] = sp.y;
         stage[5 * lane + 2] = sp.z;
         stage[5 * lane + 3] = sp.w;
-        stage[5 * lane + 4] = keep;
+        stage[5 * lane + 4] = (uint32_t)keep | ((uint32_t)wfix << 1);
       }
       const uint64_t dm = __ballot(done);
-      if (lane == 0) *dmask = dm;
-      // the commit's grid stores (watering) must land before other waves read
-      // the env's rows for its terminal info
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) {
+        *dmask = dm;
+        // one queue reservation per block (a whole batch resetting at once would
+        // otherwise serialize 65536 atomics on one address)
+        if (a.pf.scal) *qbase = atomicAdd(a.pf.qn, (uint32_t)__popcll(dm));
+      }
+      // with the curriculum, the commit's grid / visit stores of a done env
+      // (watering, the carried visit) must land before other waves read its rows
+      // (terminal info) and write new ones; otherwise it made none (see the commit)
+      if (st.cur) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
     {
@@ -613,14 +621,27 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
                                     (uint32_t)__builtin_amdgcn_readfirstlane((int)stage[5 * l + 1]),
                                     (uint32_t)__builtin_amdgcn_readfirstlane((int)stage[5 * l + 2]),
                                     (uint32_t)__builtin_amdgcn_readfirstlane((int)stage[5 * l + 3]));
-        const bool kp = __builtin_amdgcn_readfirstlane((int)stage[5 * l + 4]) != 0;
+        const int kw = __builtin_amdgcn_readfirstlane((int)stage[5 * l + 4]);
+        const bool kp = (kw & 1) != 0;
         const Scal sv = unpack(sl);
-        if (a.tinfo) coop_write_info(st, g, el, sv, a.tinfo + el * PE_NINFO, lane);
+        // the prefetched record's loads go out first, the terminal info's after them
+        PfLoad<MAXW, KD> pl;
+        if (a.pf.scal) coop_load_prefetched<MAXW, KD>(a.pf, g, el, pl, lane);
+        if (a.tinfo) coop_write_info(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, kw >> 1);
         Row4<MAXW> rw;
-        uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
-        const Scal ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane, scr);
+        Scal ns;
         asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
-        coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
+        if (a.pf.scal && coop_take_prefetched<MAXW, KD>(a.pf, g, el, sv.episode, pl, rw, ns, orow, lane)) {
+          ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane);
+        } else {
+          uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
+          ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane, scr);
+          coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
+        }
+        if (a.pf.scal && lane == 0) {  // its next map goes into the next generating batch
+          const uint32_t q = *qbase + (uint32_t)k;
+          if (q < (uint32_t)a.n) a.pf.queue[q] = (uint32_t)el;
+        }
         const uint4 np = pack(ns);
         if (lane == 0) {
           stage[5 * l] = np.x;
@@ -664,7 +685,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
     if (a.ep_ret_out) a.ep_ret_out[e] = ret;
     if (a.ep_len_out) a.ep_len_out[e] = s.step;
     PE_RSTAMP(1);
-    if (a.tinfo) write_info(a.st, a.g, ltab, e, s, a.tinfo + e * PE_NINFO);
+    if (a.tinfo) write_info(a.st, a.g, ltab, e, s, a.tinfo + e * PE_NINFO, wfix);
     PE_RSTAMP(2);
     if (!a.autoreset) {
     } else if (scratch_ok) {
@@ -905,7 +926,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
   const int xp = s.x + dxv, yp = ok ? ny : s.y;
   const uint32_t nib = n < 15u ? n + 1u : 15u;                    // :203
   float* row = rows + lane * g.D;
-  bool done = false;
+  bool done = false, wfix = false;
   if (live) {
     const int kc = dxv + R + 1;
     const int sh = 2 * (yp - yb);
@@ -920,33 +941,19 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
     }
     if (wv == CW && !(kAblate & 8)) {
       // ---- commit (plantos_env.py:160-222)
+      uint32_t wo = eo, wn = en;  // explored-bitmap words after the move (bitmap mode)
       if (ok) {
-        const int pb = (4 * (ny + 2)) & 31;
-        st_wt(st.vis + e * g.vstride + (int64_t)nx * g.NW + pbw, (vraw & ~(0xFu << pb)) | (nib << pb));
-        visit_bump_exact(st, g, e, cell_n, n);
         if (s.flags & F_EXPL_BITMAP) {                            // explored[old]=1, [new]=2 (:198-200)
           const uint32_t bo = 1u << (cell_o & 31), bn = 1u << (cell_n & 31);
-          uint32_t* ep_o = st.expl + e * g.estride + (cell_o >> 5);
-          uint32_t* ep_n = st.expl + e * g.estride + (cell_n >> 5);
           if ((cell_o >> 5) == (cell_n >> 5)) {
-            uint32_t w = eo;
-            if (!(w & bo)) { w |= bo; s.expl++; }
-            if (!(w & bn)) { w |= bn; s.expl++; }
-            if (w != eo) *ep_o = w;
+            if (!(wo & bo)) { wo |= bo; s.expl++; }
+            if (!(wo & bn)) { wo |= bn; s.expl++; }
           } else {
-            if (!(eo & bo)) { *ep_o = eo | bo; s.expl++; }
-            if (!(en & bn)) { *ep_n = en | bn; s.expl++; }
+            if (!(wo & bo)) { wo |= bo; s.expl++; }
+            if (!(wn & bn)) { wn |= bn; s.expl++; }
           }
         } else if (n == 0u) {
           s.expl++;  // derived mode: explored[new] was 0 iff never visited
-        }
-      }
-      if (watered) {
-        const int bit = 2 * (s.y + R);
-        if constexpr (ONEWORD) {
-          st_wt(const_cast<uint64_t*>(gb) + s.x, (uint64_t)(lrow[(R + 1) * EPB + lane] & ~(1ull << bit)));  // code 3 -> 2
-        } else {
-          st_wt(const_cast<uint64_t*>(gb) + (int64_t)s.x * g.WPR + (bit >> 6), (uint64_t)(craw & ~(1ull << (bit & 63))));
         }
       }
       if (bad) {
@@ -957,6 +964,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
         s.flags |= F_POISON_HYD;
         atomicOr(st.err_bits, F_POISON_HYD);
       }
+      const int ox = s.x;
       s.x = xp;                                                   // :199
       s.y = yp;
       double rew = rl.r_step;                                     // :164
@@ -968,13 +976,39 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
         s.flags |= F_BONUS;
       }
       if (st.cur) term = curriculum_hit(st.cur, e, cthr, s.expl, s.total) || term;  // A2C_training.py:101-103
+      done = term || trunc;  // terminal outputs; the reset itself only with autoreset
+      // an env about to be auto-reset gets new grid and visit rows: its last move /
+      // watering is not stored (the terminal info accounts for the watering), so no
+      // store of this step can land after the reset's (unless the curriculum
+      // carries the visits over)
+      wfix = watered && done && a.autoreset && !st.cur;
+      if (!(done && a.autoreset && !st.cur)) {
+        if (ok) {
+          const int pb = (4 * (ny + 2)) & 31;
+          st_wt(st.vis + e * g.vstride + (int64_t)nx * g.NW + pbw, (vraw & ~(0xFu << pb)) | (nib << pb));
+          visit_bump_exact(st, g, e, cell_n, n);
+          if (s.flags & F_EXPL_BITMAP) {
+            uint32_t* ep_o = st.expl + e * g.estride + (cell_o >> 5);
+            uint32_t* ep_n = st.expl + e * g.estride + (cell_n >> 5);
+            if (wo != eo) *ep_o = wo;
+            if ((cell_o >> 5) != (cell_n >> 5) && wn != en) *ep_n = wn;
+          }
+        }
+        if (watered) {
+          const int bit = 2 * (s.y + R);
+          if constexpr (ONEWORD) {
+            st_wt(const_cast<uint64_t*>(gb) + ox, (uint64_t)(lrow[(R + 1) * EPB + lane] & ~(1ull << bit)));  // code 3 -> 2
+          } else {
+            st_wt(const_cast<uint64_t*>(gb) + (int64_t)ox * g.WPR + (bit >> 6), (uint64_t)(craw & ~(1ull << (bit & 63))));
+          }
+        }
+      }
       ret += rew;
       st_wt(a.reward + e, (float)rew);
       st_wt(a.term + e, (uint8_t)term);
       st_wt(a.trunc + e, (uint8_t)trunc);
       st_wt(st.ep_ret + e, ret);
       st_wt(st.scal + e, pack(s));
-      done = term || trunc;  // terminal outputs; the reset itself only with autoreset
     }
   }
   PE_STAMP(4);
@@ -993,8 +1027,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
   static_assert(2 * C * R <= (NR * 8 + NV * 4) * EPB, "LIDAR offset tables must fit the window region");
   static_assert(5 * 4 * EPB + 8 <= (NR * 8 + NV * 4) * EPB, "reset staging must fit the window region");
   if (__builtin_expect(any_done, 0)) {  // cold: laid out after the hot path
-    const uint4 ns = quad_done_path<NW, ONEWORD>(kernargs(), quad_tile_off<R>(), C, R, lane, wv, CW, e0, done,
-                                                 pack(s), ret, ndone);
+    const uint4 ns = quad_done_path<NW, ONEWORD, (5 * C + 27 + 63) / 64>(kernargs(), quad_tile_off<R>(), C, R, lane, wv, CW, e0, done,
+                                                 pack(s), ret, ndone, wfix);
     s = unpack(ns);
   }
   const int64_t valid = a.n - e0 < EPB ? a.n - e0 : EPB;
@@ -1046,6 +1080,48 @@ __global__ __launch_bounds__(256) void pe_reset_coop_kernel(StepArgs a) {
     if (a.obs) coop_fresh_obs<MAXW>(g, rw, ns, a.obs + e * g.D, tdist, tpos, tvis, a.st.ldx, a.st.ldy, lane);
   } else if (a.obs && lane == 0) {
     build_obs_generic(a, e, s.x, s.y, a.obs + e * g.D, tdist, tpos, tvis, a.st.ldx, a.st.ldy);
+  }
+}
+
+// Prefetched resets (pe_coop.hpp Prefetch): generate the next reset's map, grid
+// rows and fresh obs of the envs queued by the step kernel (all == 0; grid-stride
+// over the queue, then the last workgroup clears the queue), or of every env
+// (all != 0: one wave per env; after create / reset()), skipping envs whose
+// record already holds the reset of their current episode counter.
+template <int MAXW>
+__global__ __launch_bounds__(256) void pe_prefetch_kernel(StepArgs a, int all) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const Geo& g = a.g;
+  const Prefetch& pf = a.pf;
+  const uint32_t queued = all ? 0u : (uint32_t)__builtin_amdgcn_readfirstlane((int)pf.qn[0]);
+  if (!all && queued == 0u) return;  // nothing queued (the usual launch between synchronized resets)
+  load_tables(smem, a.st.tab);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = (int64_t)gridDim.x * 4;
+  uint64_t* scr = reinterpret_cast<uint64_t*>(smem + kTabFloats) + (threadIdx.x >> 6) * coop_scratch_words(g.G, g.WPR);
+  const int64_t cnt = all ? (int64_t)a.n : (int64_t)(queued < (uint32_t)a.n ? queued : (uint32_t)a.n);
+  for (int64_t i = wid; i < cnt; i += nwaves) {
+    const int64_t e = all ? i : (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)pf.queue[i]);
+    const uint32_t ep = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.st.scal[e].w);
+    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)pf.scal[e].w) == ep + 1u) continue;  // already there
+    Row4<MAXW> rw;
+    const Scal s = coop_gen_map<MAXW>(g, a.rl, a.st.tab, rw, a.rl.env_off + (uint32_t)e, ep, lane, scr);
+    if (lane < g.G) {
+      uint64_t* dst = pf.grid + e * g.gstride + (int64_t)lane * g.WPR;
+#pragma unroll
+      for (int w = 0; w < MAXW; ++w)
+        if (MAXW == 1 || w < g.WPR) dst[w] = rw.get(w);
+    }
+    coop_fresh_obs<MAXW>(g, rw, s, pf.obs + e * g.D, smem, smem + 72, smem + 328, a.st.ldx, a.st.ldy, lane);
+    if (lane == 0) pf.scal[e] = pack(s);  // read by a later launch only
+  }
+  if (!all) {
+    __syncthreads();  // every wave of this workgroup has read the count
+    if (threadIdx.x == 0 && atomicAdd(pf.qn + 1, 1u) == gridDim.x - 1) {
+      pf.qn[0] = 0u;  // the last workgroup: nobody reads the count any more
+      pf.qn[1] = 0u;
+    }
   }
 }
 
@@ -1345,6 +1421,7 @@ StepArgs base_args(const pe_handle* h) {
   a.autoreset = h->cfg.autoreset;
   a.stagger = h->stagger;
   a.coop_max_done = h->coop_max_done;
+  a.pf = h->pf;
   return a;
 }
 
@@ -1394,6 +1471,23 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
       default: hipLaunchKernelGGL(pe_step_kernel, grid, block, lds, s, a); break;
     }
   }
+  PE_HIP(hipGetLastError());
+  return PE_OK;
+}
+
+// The prefetch launches (pe_prefetch_kernel): queue mode on one resident grid
+// (h->pf_blocks: every workgroup the chip holds at once; a steady-state batch of K
+// steps' resets, ~65 K envs at 65536 envs, is about one map per wave), all mode
+// with one wave per env.
+int launch_prefetch(const pe_handle* h, hipStream_t s, int all) {
+  StepArgs a = base_args(h);
+  const unsigned nb = (unsigned)((h->n + 3) / 4);
+  dim3 grid(all ? nb : std::min(nb, (unsigned)h->pf_blocks)), block(256);
+  const size_t lds = sizeof(float) * (size_t)kTabFloats + 4 * 8 * (size_t)coop_scratch_words(h->g.G, h->g.WPR);
+  if (h->g.WPR == 1)
+    hipLaunchKernelGGL(pe_prefetch_kernel<1>, grid, block, lds, s, a, all);
+  else
+    hipLaunchKernelGGL(pe_prefetch_kernel<kCoopWPR>, grid, block, lds, s, a, all);
   PE_HIP(hipGetLastError());
   return PE_OK;
 }
@@ -1559,7 +1653,6 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
     h->coop_max_done = kCoopMaxDone;
   else
     h->coop_max_done = kQuadEnvs;
-  if (const char* cm = std::getenv("PE_COOP_MAX_DONE")) h->coop_max_done = std::atoi(cm);  // A/B
   rl.max_steps = c->max_steps;
 
   // host tables
@@ -1597,6 +1690,14 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   if (is_quad(h->variant) && quad_lds_bytes(g) > 160 * 1024) h->variant -= V_QUAD_C16R6_1W - V_C16R6_1W;
   if (h->variant == V_QUAD_C16R6_1W && g.NW != 4) h->variant = V_C16R6_1W;  // needs 16-B visit rows
   h->kname = variant_name(h->variant);
+  // Prefetched resets (pe_coop.hpp Prefetch) where the sector kernel takes the
+  // cooperative path: the in-kernel reset is then a copy, so it wins even when a
+  // whole block is done at once.
+  const char* pfe = std::getenv("PE_PREFETCH_EVERY");
+  h->pf_every = pfe ? std::atoi(pfe) : kPrefetchEvery;
+  if (!is_quad(h->variant) || h->coop_max_done <= 0 || !c->autoreset) h->pf_every = 0;
+  if (h->pf_every > 0) h->coop_max_done = kQuadEnvs;
+  if (const char* cm = std::getenv("PE_COOP_MAX_DONE")) h->coop_max_done = std::atoi(cm);  // A/B
   const char* qw = std::getenv("PE_QUAD_WAVES");
   // measured (profiles/r1c-r1e): 4 waves win at C=16, 8 waves at C=64
   h->quad_waves = qw ? (std::atoi(qw) == 8 ? 8 : 4) : 4;  // 4 measured best at C=16 and C=64
@@ -1643,6 +1744,37 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   h->st.vx = reinterpret_cast<uint32_t*>(base + o_vx);
   h->st.expl = reinterpret_cast<uint32_t*>(base + o_expl);
   int rc = PE_OK;
+  if (h->pf_every > 0) {
+    size_t po = 0;
+    auto pcarve = [&](size_t bytes) {
+      size_t o = po;
+      po = align_up(po + bytes, 256);
+      return o;
+    };
+    const size_t p_scal = pcarve(n * sizeof(uint4)), p_grid = pcarve(n * (size_t)g.gstride * 8);
+    const size_t p_obs = pcarve(n * (size_t)g.D * 4), p_q = pcarve(n * 4), p_qn = pcarve(2 * 4);
+    if (hipMalloc(&h->pf_mem, po) != hipSuccess || hipMemset(h->pf_mem, 0, po) != hipSuccess) {
+      if (h->pf_mem) (void)hipFree(h->pf_mem);
+      (void)hipFree(h->mem);
+      delete[] ldx;
+      delete[] ldy;
+      delete h;
+      return fail(PE_ERR_NOMEM, "prefetch buffers: hipMalloc failed");
+    }
+    char* pb = static_cast<char*>(h->pf_mem);
+    h->pf.scal = reinterpret_cast<uint4*>(pb + p_scal);
+    h->pf.grid = reinterpret_cast<uint64_t*>(pb + p_grid);
+    h->pf.obs = reinterpret_cast<float*>(pb + p_obs);
+    h->pf.queue = reinterpret_cast<uint32_t*>(pb + p_q);
+    h->pf.qn = reinterpret_cast<uint32_t*>(pb + p_qn);
+    const size_t plds = sizeof(float) * (size_t)kTabFloats + 4 * 8 * (size_t)coop_scratch_words(G, g.WPR);
+    int per_cu = 0;
+    hipError_t oe = g.WPR == 1
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pe_prefetch_kernel<1>, 256, plds)
+        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pe_prefetch_kernel<kCoopWPR>, 256, plds);
+    if (oe != hipSuccess || per_cu < 1) per_cu = 1;
+    h->pf_blocks = per_cu * prop.multiProcessorCount;
+  }
   hipError_t e1 = hipMemset(h->mem, 0, h->bytes);
   hipError_t e2 = hipMemcpy(base + o_tab, &tab, sizeof(Tables), hipMemcpyHostToDevice);
   hipError_t e3 = hipMemcpy(base + o_ldx, ldx, nl, hipMemcpyHostToDevice);
@@ -1650,6 +1782,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   delete[] ldx;
   delete[] ldy;
   if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess) {
+    if (h->pf_mem) (void)hipFree(h->pf_mem);
     (void)hipFree(h->mem);
     delete h;
     return fail(PE_ERR_DEVICE, "initial upload failed");
@@ -1657,11 +1790,13 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   // every env starts reset (episode 0), like DummyVecEnv.reset() before the first step
   StepArgs a = base_args(h);
   rc = launch_reset(h, a, nullptr);
+  if (rc == PE_OK && h->pf_every > 0) rc = launch_prefetch(h, nullptr, 1);
   if (rc == PE_OK) {
     hipError_t se = hipDeviceSynchronize();
     if (se != hipSuccess) rc = hip_fail(se, "initial reset");
   }
   if (rc != PE_OK) {
+    if (h->pf_mem) (void)hipFree(h->pf_mem);
     (void)hipFree(h->mem);
     delete h;
     return rc;
@@ -1679,6 +1814,7 @@ int pe_destroy(pe_handle* h) {
     if (e != hipSuccess) rc = hip_fail(e, "hipFree");
   }
   if (h->cur_mem) (void)hipFree(h->cur_mem);
+  if (h->pf_mem) (void)hipFree(h->pf_mem);
   delete h;
   return rc;
 }
@@ -1731,11 +1867,13 @@ int pe_curriculum_get(pe_handle* h, double* threshold, int32_t* counters, void* 
 
 int pe_seed(pe_handle* h, uint64_t seed, int32_t reset_episode_counters) {
   if (!h) return fail(PE_ERR_ARG, "null handle");
+  DeviceGuard dg(h);
+  if (dg.rc) return dg.rc;
+  if (h->pf.scal && seed != h->rl.seed)  // every prefetched map belongs to the old seed
+    PE_HIP(hipMemset(h->pf.scal, 0, sizeof(uint4) * (size_t)h->n));
   h->rl.seed = seed;
   h->cfg.seed = seed;
   if (reset_episode_counters) {
-    DeviceGuard dg(h);
-    if (dg.rc) return dg.rc;
     // the episode counter is the 4th word of each packed scalar record
     PE_HIP(hipMemset2D(reinterpret_cast<char*>(h->st.scal) + 12, sizeof(uint4), 0, 4, (size_t)h->n));
   }
@@ -1749,7 +1887,9 @@ int pe_reset(pe_handle* h, const uint8_t* mask, float* obs, void* stream) {
   StepArgs a = base_args(h);
   a.mask = mask;
   a.obs = obs;
-  return launch_reset(h, a, static_cast<hipStream_t>(stream));
+  const int rc = launch_reset(h, a, static_cast<hipStream_t>(stream));
+  if (rc != PE_OK || h->pf_every <= 0) return rc;
+  return launch_prefetch(h, static_cast<hipStream_t>(stream), 1);  // the new episodes' next maps
 }
 
 int pe_step(pe_handle* h, const void* actions, int32_t action_bytes, float* obs, float* reward, uint8_t* terminated,
@@ -1770,7 +1910,10 @@ int pe_step(pe_handle* h, const void* actions, int32_t action_bytes, float* obs,
   a.ep_ret_out = ep_ret;
   a.ep_len_out = ep_len;
   a.tinfo = terminal_info;
-  return launch_step(h, a, static_cast<hipStream_t>(stream));
+  const int rc = launch_step(h, a, static_cast<hipStream_t>(stream));
+  if (rc != PE_OK || h->pf_every <= 0 || ++h->pf_count < h->pf_every) return rc;
+  h->pf_count = 0;
+  return launch_prefetch(h, static_cast<hipStream_t>(stream), 0);  // maps for the envs reset since the last one
 }
 
 int pe_get_info(pe_handle* h, int32_t* info, void* stream) {

@@ -1,8 +1,9 @@
 """GPU parity of the step kernel's auto-reset paths against the oracle with
 DESYNCHRONIZED episodes (every env starts at its own step count, so a few envs
-reset in every step, as in steady-state training): the wave-cooperative reset
-(pe_coop.hpp: sparse resets, and every reset at 64x64) and, forced through
-PE_COOP_MAX_DONE, both paths for dense resets.  Every output of every step is
+reset in every step, as in steady-state training): prefetched resets (maps
+generated ahead by pe_prefetch_kernel, at several launch cadences, across a seed
+change), the wave-cooperative reset (pe_coop.hpp) and, forced through
+PE_COOP_MAX_DONE / PE_PREFETCH_EVERY, every path for dense resets.  Every output of every step is
 compared, plus the terminal info rows and the final state.
 """
 import numpy as np
@@ -36,21 +37,30 @@ def info_rows(b, idx):
     return rows
 
 
-@pytest.mark.parametrize("name,n,steps,spread,coop_max", [
-    ("g20", 2048, 160, 150, None),   # sparse: cooperative resets
-    ("g64", 192, 50, 40, None),      # 64x64: cooperative resets always
-    ("g7", 700, 120, 100, None),
-    ("g32", 300, 60, 50, None),
-    ("g21", 400, 60, 50, None),
-    ("g20", 256, 12, 1, "64"),       # every env at once, forced through the cooperative path
-    ("g64", 128, 12, 1, "0"),        # every env at once, forced through the lane-per-env path
+@pytest.mark.parametrize("name,n,steps,spread,coop_max,every,reseed_at", [
+    ("g20", 2048, 160, 150, None, None, None),   # sparse: prefetched / cooperative resets
+    ("g64", 192, 50, 40, None, None, None),      # 64x64: cooperative resets always
+    ("g7", 700, 120, 100, None, None, None),
+    ("g32", 300, 60, 50, None, None, None),
+    ("g21", 400, 60, 50, None, None, None),
+    ("g20", 256, 12, 1, "64", None, None),       # every env at once through the cooperative path
+    ("g64", 128, 12, 1, "0", None, None),        # every env at once through the lane-per-env path
+    ("g20", 256, 12, 1, "8", "0", None),         # no prefetch: in-kernel map generation
+    ("g20", 1024, 80, 60, None, "1", None),      # prefetch launch after every step
+    ("g20", 1024, 80, 60, None, "7", None),
+    ("g32", 300, 60, 50, None, "0", None),
+    ("g20", 1024, 80, 60, None, "5", 30),        # new seed mid-run: prefetched maps dropped
+    ("g64", 192, 40, 30, None, "3", 15),
 ])
-def test_desync_autoreset_parity(name, n, steps, spread, coop_max, monkeypatch):
+def test_desync_autoreset_parity(name, n, steps, spread, coop_max, every, reseed_at, monkeypatch):
+    """every: PE_PREFETCH_EVERY (steps between prefetch launches; "0" = off)."""
     from plantos_amd import PlantOSBatch
     if coop_max is not None:
         monkeypatch.setenv("PE_COOP_MAX_DONE", coop_max)
+    if every is not None:
+        monkeypatch.setenv("PE_PREFETCH_EVERY", every)
     G, P, Ob, R, C = cfg = CFG[name]
-    seed = 31
+    seed = aseed = 31
     b = PlantOSBatch(n, grid_size=G, num_plants=P, num_obstacles=Ob, lidar_range=R, lidar_channels=C, seed=seed,
                      device="cuda:0")
     ov = OracleVec(cfg, np.arange(n), seed)
@@ -64,7 +74,10 @@ def test_desync_autoreset_parity(name, n, steps, spread, coop_max, monkeypatch):
     act = torch.empty(n, dtype=torch.int32, device="cuda:0")
     resets = 0
     for t in range(steps):
-        b.synth_actions(seed, t, out=act)
+        if t == reseed_at:  # map stream of every later reset keyed by the new seed
+            seed = 977
+            b.seed(seed, reset_episode_counters=False)
+        b.synth_actions(aseed, t, out=act)
         a_np = np_(act)
         obs, rew, te, tr = b.step(act)
         # oracle: step, pre-reset info of the done envs, then the resets (OracleVec.step)

@@ -20,9 +20,13 @@ def main():
     acts = torch.empty((64, n), dtype=torch.int32, device="cuda:0")
     for t in range(64):
         b.synth_actions(0, t, out=acts[t])
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    for t in range(998):
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    for t in range(934):
         b.step(acts[t % 64])
+    ev[3].record()
+    for t in range(934, 998):
+        b.step(acts[t % 64])
+    ev[4].record()
     torch.cuda.synchronize()
     ev[0].record()
     b.step(acts[998 % 64])
@@ -31,6 +35,18 @@ def main():
     ev[2].record()
     torch.cuda.synchronize()
     tr = b.truncated.float().mean().item()
+    # the 64 steps from the reset on (incl. a prefetch launch regenerating every
+    # env's next map, when prefetching) vs 64 plain steps
+    w0 = torch.cuda.Event(enable_timing=True)
+    w1 = torch.cuda.Event(enable_timing=True)
+    b.step(acts[0])
+    torch.cuda.synchronize()
+    w0.record()
+    for t in range(1001, 1065):
+        b.step(acts[t % 64])
+    w1.record()
+    torch.cuda.synchronize()
+    win_after = w0.elapsed_time(w1) + ev[1].elapsed_time(ev[2])
     t0 = torch.cuda.Event(enable_timing=True)
     t1 = torch.cuda.Event(enable_timing=True)
     t0.record()
@@ -39,6 +55,7 @@ def main():
     torch.cuda.synchronize()
     print(json.dumps({"kernel": b.kernel_name, "grid": G, "plain_step_ms": ev[0].elapsed_time(ev[1]),
                       "reset_step_ms": ev[1].elapsed_time(ev[2]), "truncated_frac": tr,
+                      "plain_64_steps_ms": ev[3].elapsed_time(ev[4]), "reset_plus_64_steps_ms": win_after,
                       "pe_reset_all_ms": t0.elapsed_time(t1)}))
 
 
