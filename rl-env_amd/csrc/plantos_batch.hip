@@ -593,7 +593,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
       if (lane == 0) {
         *dmask = dm;
         // one queue reservation per block (a whole batch resetting at once would
-        // otherwise serialize 65536 atomics on one address)
+        // otherwise serialize 65536 atomics on one word)
         if (a.pf.scal) *qbase = atomicAdd(a.pf.qn, (uint32_t)__popcll(dm));
       }
       // with the curriculum, the commit's grid / visit stores of a done env
@@ -1020,8 +1020,16 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
     const uint64_t dm = __ballot(done);
     if (lane == 0) reinterpret_cast<uint64_t*>(smem)[35] = dm;
   }
-  const bool any_done = __syncthreads_or(done);
-  const int ndone = any_done ? __popcll(reinterpret_cast<const uint64_t*>(smem)[35]) : 0;
+  // The block barrier (obs rows and the done mask complete in LDS) WITHOUT a memory
+  // fence: __syncthreads() would make the commit wave wait for its state stores to
+  // land first (s_waitcnt vmcnt(0)), although nothing in this launch reads them
+  // back -- the reset path orders its own accesses (see quad_done_path).
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  const uint64_t dmask = reinterpret_cast<const uint64_t*>(smem)[35];  // after the asm barrier ("memory")
+  const uint64_t dmu = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)dmask) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(dmask >> 32)) << 32);
+  const bool any_done = dmu != 0ull;
+  const int ndone = __popcll(dmu);
   PE_STAMP(5);
   // auto-reset slow path, out of line (its registers stay off the hot path)
   static_assert(2 * C * R <= (NR * 8 + NV * 4) * EPB, "LIDAR offset tables must fit the window region");
