@@ -214,8 +214,12 @@ __device__ __forceinline__ void load_tables_cold(float* smem, const Tables* tab)
 }
 
 // Stream the block's [valid x D] obs tile (LDS rows of stride DS) to HBM.
-__device__ __forceinline__ void store_tile(const float* rows, float* dst, int valid, int D, int DS) {
+// t0 / nt: this thread's index among the nt storing threads (default: the block).
+__device__ __forceinline__ void store_tile(const float* rows, float* dst, int valid, int D, int DS,
+                                           int t0 = -1, int nt = 0) {
   const int total = valid * D;
+  const int tid = t0 < 0 ? (int)threadIdx.x : t0;
+  const int nth = t0 < 0 ? (int)blockDim.x : nt;
   if (DS == D) {
     if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
       const int n4 = total >> 2;
@@ -232,7 +236,7 @@ __device__ __forceinline__ void store_tile(const float* rows, float* dst, int va
       // compiler does not count these in vmcnt; the reset path waits explicitly.
       typedef float v4f __attribute__((ext_vector_type(4)));
       const v4f* sv = reinterpret_cast<const v4f*>(rows);
-      for (int k = threadIdx.x; k < n4; k += blockDim.x) {
+      for (int k = tid; k < n4; k += nth) {
         const v4f v = sv[k];
         // s_nop 1: a 128-bit store reads its data VGPRs after issue; nothing inside
         // the asm pads that hazard for hipcc's next write of them
@@ -243,16 +247,16 @@ __device__ __forceinline__ void store_tile(const float* rows, float* dst, int va
       typedef float v4f __attribute__((ext_vector_type(4)));
       const v4f* sv = reinterpret_cast<const v4f*>(rows);
       v4f* dv = reinterpret_cast<v4f*>(dst);
-      for (int k = threadIdx.x; k < n4; k += blockDim.x) __builtin_nontemporal_store(sv[k], &dv[k]);
+      for (int k = tid; k < n4; k += nth) __builtin_nontemporal_store(sv[k], &dv[k]);
 #else
-      for (int k = threadIdx.x; k < n4; k += blockDim.x) d4[k] = s4[k];
+      for (int k = tid; k < n4; k += nth) d4[k] = s4[k];
 #endif
-      for (int k = (n4 << 2) + threadIdx.x; k < total; k += blockDim.x) dst[k] = rows[k];
+      for (int k = (n4 << 2) + tid; k < total; k += nth) dst[k] = rows[k];
     } else {
-      for (int k = threadIdx.x; k < total; k += blockDim.x) dst[k] = rows[k];
+      for (int k = tid; k < total; k += nth) dst[k] = rows[k];
     }
   } else {
-    for (int k = threadIdx.x; k < total; k += blockDim.x) {
+    for (int k = tid; k < total; k += nth) {
       int r = k / D, c = k - r * D;
       dst[k] = rows[r * DS + c];
     }
@@ -657,6 +661,11 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
       st.ep_ret[e] = 0.0;
       st.scal[e] = pack(s);
     }
+    // vmcnt(0) as an instruction the compiler tracks (not asm): nothing of this path
+    // is pending where it rejoins the hot path, so the tile store loop after it
+    // carries no per-iteration wait (only the commit wave waits here, and it does
+    // not take part in the tile store)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
     return pack(s);
   }
   // Many done envs (a synchronized batch truncating together): one lane per env.
@@ -1040,7 +1049,12 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
     s = unpack(ns);
   }
   const int64_t valid = a.n - e0 < EPB ? a.n - e0 : EPB;
-  if constexpr (!(kAblate & 1)) store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D);
+  // the obs tile goes out through the waves other than the commit wave: its state
+  // stores are still in flight (no fence at the barrier above), and the compiler
+  // would make every iteration of its store loop wait for them (s_waitcnt vmcnt(0)
+  // before re-using a store's data registers)
+  if constexpr (!(kAblate & 1))
+    if (wv != CW) store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D, (int)threadIdx.x, 64 * (NW - 1));
   if (any_done && a.autoreset && !quad_coop(a, ndone) && reset_scratch_bytes(g.G, g.WPR, rl.P) <= 4 * g.D) {
     // the tile store above wrote scratch bytes into the done rows: drain it, then
     // overwrite those rows with the fresh obs built from the LDS grid image
