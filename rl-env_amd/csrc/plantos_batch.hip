@@ -818,40 +818,56 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
     const int lx = (int)(lw.x & 0xFF), ly = (int)((lw.x >> 8) & 0xFF);
     const uint64_t* lgb = st.grid + el * g.gstride;
     const int base = lx - R - 1;  // grid row of LDS row 0
+    // Every load first, then the LDS writes: the loads are unconditional (row
+    // indices clamped into the map, off-map rows selected away afterwards), so the
+    // compiler issues all of them back to back and waits once -- with the range
+    // tests around the loads it waited after each (one memory round trip per row).
     if constexpr (ONEWORD) {
       // row pairs (16 B, aligned: env blocks are 16-B aligned, pairs start on even rows)
       const int ps = base & ~1;
-      constexpr int NP = (NR + 2) / 2;
+      constexpr int NP = (NR + 2) / 2, JG = (NP + LT - 1) / LT, JV = (NV + LT - 1) / LT;
+      const int gmax = g.G - 2 > 0 ? g.G - 2 : 0;
+      uint4 qg[JG], qv[JV];
 #pragma unroll
-      for (int j = 0; j < (NP + LT - 1) / LT; ++j) {
+      for (int j = 0; j < JG; ++j) {
+        const int ra = ps + 2 * (sub + LT * j);
+        const int rc = ra < 0 ? 0 : (ra > gmax ? gmax : ra);
+        qg[j] = *reinterpret_cast<const uint4*>(lgb + rc);
+      }
+      const uint32_t* lvb = st.vis + el * g.vstride;
+#pragma unroll
+      for (int j = 0; j < JV; ++j) {
+        const int xr = lx - 3 + sub + LT * j;
+        const int xc = xr < 0 ? 0 : (xr >= g.G ? g.G - 1 : xr);
+        qv[j] = *reinterpret_cast<const uint4*>(lvb + (int64_t)xc * 4);  // g.NW == 4
+      }
+#pragma unroll
+      for (int j = 0; j < JG; ++j) {
         const int pp = sub + LT * j;
         if (pp < NP && !(kAblate & 32)) {
           const int ra = ps + 2 * pp;
-          uint64_t va = kEven64, vb2 = kEven64;  // off-map rows: obstacles
-          if (ra >= 0 && ra + 1 < g.G) {
-            const uint4 q = *reinterpret_cast<const uint4*>(lgb + ra);
-            va = (uint64_t)q.x | ((uint64_t)q.y << 32);
-            vb2 = (uint64_t)q.z | ((uint64_t)q.w << 32);
-          } else {
-            if (ra >= 0 && ra < g.G) va = lgb[ra];
-            if (ra + 1 >= 0 && ra + 1 < g.G) vb2 = lgb[ra + 1];
-          }
+          const int rc = ra < 0 ? 0 : (ra > gmax ? gmax : ra);
+          const uint64_t lo = (uint64_t)qg[j].x | ((uint64_t)qg[j].y << 32);
+          const uint64_t hi = (uint64_t)qg[j].z | ((uint64_t)qg[j].w << 32);
+          // off-map rows: obstacles
+          const uint64_t va = (ra >= 0 && ra < g.G) ? (ra == rc ? lo : hi) : kEven64;
+          const uint64_t vb2 = (ra + 1 >= 0 && ra + 1 < g.G) ? (ra + 1 == rc ? lo : hi) : kEven64;
           const int ka = ra - base;
           if (ka >= 0 && ka < NR) lrow[ka * EPB + le] = va;
           if (ka + 1 >= 0 && ka + 1 < NR) lrow[(ka + 1) * EPB + le] = vb2;
         }
       }
-      // visit rows: one 16-B row per load (g.NW == 4), funnel-shifted to ybv
+      // visit rows: one 16-B row per load, funnel-shifted to ybv
       const int lybv = ly > 0 ? ly - 1 : 0;
       const int vw = (4 * lybv) >> 5, vo = (4 * lybv) & 31;
 #pragma unroll
-      for (int j = 0; j < (NV + LT - 1) / LT; ++j) {
+      for (int j = 0; j < JV; ++j) {
         const int k = sub + LT * j;
         if (k < NV && !(kAblate & 16)) {
           const int xr = lx - 3 + k;
           uint32_t lo = 0xAAAAAAAAu, hi = 0xAAAAAAAAu;  // off-map row: visit 10 (reads 1.0)
           if (xr >= 0 && xr < g.G) {
-            const uint4 q = *reinterpret_cast<const uint4*>(st.vis + el * g.vstride + (int64_t)xr * 4);
+            const uint4 q = qv[j];
             lo = vw == 0 ? q.x : (vw == 1 ? q.y : q.z);
             hi = vw == 0 ? q.y : (vw == 1 ? q.z : q.w);
           }
@@ -861,23 +877,50 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArg
     } else {
       const int lyb = ly > 0 ? ly - 1 : 0;
       const int w0 = (2 * lyb) >> 6, o = (2 * lyb) & 63;
+      const int w1 = w0 + 1 < g.WPR ? w0 + 1 : w0;  // in bounds; its word is dropped when w0 is the last
+      constexpr int JG = (NR + LT - 1) / LT, JV = (NV + LT - 1) / LT;
+      uint64_t glo[JG], ghi[JG];
+      uint32_t vlo[JV], vhi[JV];
 #pragma unroll
-      for (int j = 0; j < (NR + LT - 1) / LT; ++j) {
-        const int k = sub + LT * j;
-        if (k < NR) lrow[k * EPB + le] = quad_row<false>(lgb, g, base + k, w0, o);
+      for (int j = 0; j < JG; ++j) {
+        const int xr = base + sub + LT * j;
+        const int xc = xr < 0 ? 0 : (xr >= g.G ? g.G - 1 : xr);
+        const uint64_t* p = lgb + (int64_t)xc * g.WPR;
+        glo[j] = p[w0];
+        ghi[j] = p[w1];
       }
       const int lybv = ly > 0 ? ly - 1 : 0;
       const int vw = (4 * lybv) >> 5, vo = (4 * lybv) & 31;
       const uint32_t* vb = st.vis + el * g.vstride + vw;
 #pragma unroll
-      for (int j = 0; j < (NV + LT - 1) / LT; ++j) {
+      for (int j = 0; j < JV; ++j) {
+        const int xr = lx - 3 + sub + LT * j;
+        const int xc = xr < 0 ? 0 : (xr >= g.G ? g.G - 1 : xr);
+        vlo[j] = vb[(int64_t)xc * g.NW];
+        vhi[j] = vb[(int64_t)xc * g.NW + 1];  // vw + 1 < NW always (one spare word per row)
+      }
+#pragma unroll
+      for (int j = 0; j < JG; ++j) {
+        const int k = sub + LT * j;
+        if (k < NR) {
+          const int xr = base + k;
+          uint64_t v = kEven64;  // off-map rows read as obstacles
+          if (xr >= 0 && xr < g.G) {
+            const uint64_t hi = w0 + 1 < g.WPR ? ghi[j] : 0ull;
+            v = o ? ((glo[j] >> o) | (hi << (64 - o))) : glo[j];
+          }
+          lrow[k * EPB + le] = v;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < JV; ++j) {
         const int k = sub + LT * j;
         if (k < NV) {
           const int xr = lx - 3 + k;
           uint32_t lo = 0xAAAAAAAAu, hi = 0xAAAAAAAAu;
           if (xr >= 0 && xr < g.G) {
-            lo = vb[(int64_t)xr * g.NW];
-            hi = vb[(int64_t)xr * g.NW + 1];
+            lo = vlo[j];
+            hi = vhi[j];
           }
           lvis[k * EPB + le] = vo ? ((lo >> vo) | (hi << (32 - vo))) : lo;
         }
