@@ -568,6 +568,61 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
   float* row = rows + lane * g.D;
   const int64_t e = e0 + lane;
   Scal s = unpack(sp);
+  constexpr int MAXW = ONEWORD ? 1 : kCoopWPR;
+  if (ndone == 1 && quad_coop(a, ndone)) {
+    // One done env (the usual case with desynchronized episodes): the commit wave,
+    // which holds its scalars, resets it alone -- no staging, one barrier.
+    if (wv == CW) {
+      const uint64_t dmw = reinterpret_cast<const uint64_t*>(smem)[35];
+      const int l = __ffsll((unsigned long long)dmw) - 1;
+      const int64_t el = e0 + l;
+      float* orow = rows + l * g.D;
+      PfLoad<MAXW, KD> pl;
+      if (a.pf.scal) coop_load_prefetched<MAXW, KD>(a.pf, g, el, pl, lane);  // in flight from here on
+      bool keep = false;
+      if (done) {
+        if (a.ep_ret_out) a.ep_ret_out[e] = ret;
+        if (a.ep_len_out) a.ep_len_out[e] = s.step;
+        if (st.cur) keep = curriculum_on_reset(st.cur, e, rl);  // A2C_training.py:56-95
+      }
+      const bool kp = __builtin_amdgcn_readlane((int)keep, l) != 0;
+      const int wf = __builtin_amdgcn_readlane((int)wfix, l);
+      const Scal sv = unpack(make_uint4((uint32_t)__builtin_amdgcn_readlane((int)sp.x, l),
+                                        (uint32_t)__builtin_amdgcn_readlane((int)sp.y, l),
+                                        (uint32_t)__builtin_amdgcn_readlane((int)sp.z, l),
+                                        (uint32_t)__builtin_amdgcn_readlane((int)sp.w, l)));
+      if (a.tobs) {
+        float* t = a.tobs + el * g.D;
+        for (int k2 = lane; k2 < g.D; k2 += 64) t[k2] = orow[k2];
+      }
+      // with the curriculum the commit stored this env's rows: they must land before
+      // the info reads them and the reset rewrites them
+      if (st.cur) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (a.tinfo) coop_write_info(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, wf);
+      Row4<MAXW> rw;
+      Scal ns;
+      asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
+      if (a.pf.scal && coop_take_prefetched<MAXW, KD>(a.pf, g, el, sv.episode, pl, rw, ns, orow, lane)) {
+        ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane);
+      } else {
+        uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
+        ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane, scr);
+        coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
+      }
+      if (a.pf.scal && lane == 0) {  // its next map goes into the next generating batch
+        const uint32_t q = atomicAdd(a.pf.qn, 1u);
+        if (q < (uint32_t)a.n) a.pf.queue[q] = (uint32_t)el;
+      }
+      if (done) {  // lane l: program order after its commit stores
+        s = ns;
+        st.ep_ret[e] = 0.0;
+        st.scal[e] = pack(s);
+      }
+    }
+    __syncthreads();  // the fresh obs row is in the tile
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // see the end of the path below
+    return pack(s);
+  }
   if (quad_coop(a, ndone)) {
     // A few done envs: wave-cooperative resets (pe_coop.hpp), spread over the
     // block's waves (the k-th done env to wave k % NW).  For each, the 64 lanes
@@ -607,7 +662,6 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
     }
     __syncthreads();
     {
-      constexpr int MAXW = ONEWORD ? 1 : kCoopWPR;
       const uint64_t dml = *dmask;  // uniform: read into scalar registers
       uint64_t dm = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)dml) |
                     ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(dml >> 32)) << 32);
