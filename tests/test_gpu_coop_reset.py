@@ -37,22 +37,24 @@ def info_rows(b, idx):
     return rows
 
 
-@pytest.mark.parametrize("name,n,steps,spread,coop_max,every,reseed_at", [
-    ("g20", 2048, 160, 150, None, None, None),   # sparse: prefetched / cooperative resets
-    ("g64", 192, 50, 40, None, None, None),      # 64x64: cooperative resets always
-    ("g7", 700, 120, 100, None, None, None),
-    ("g32", 300, 60, 50, None, None, None),
-    ("g21", 400, 60, 50, None, None, None),
-    ("g20", 256, 12, 1, "64", None, None),       # every env at once through the cooperative path
-    ("g64", 128, 12, 1, "0", None, None),        # every env at once through the lane-per-env path
-    ("g20", 256, 12, 1, "8", "0", None),         # no prefetch: in-kernel map generation
-    ("g20", 1024, 80, 60, None, "1", None),      # prefetch launch after every step
-    ("g20", 1024, 80, 60, None, "7", None),
-    ("g32", 300, 60, 50, None, "0", None),
-    ("g20", 1024, 80, 60, None, "5", 30),        # new seed mid-run: prefetched maps dropped
-    ("g64", 192, 40, 30, None, "3", 15),
+@pytest.mark.parametrize("name,n,steps,spread,coop_max,every,reseed_at,reset_at", [
+    ("g20", 2048, 160, 150, None, None, None, None),   # sparse: prefetched / cooperative resets
+    ("g64", 192, 50, 40, None, None, None, None),      # 64x64: cooperative resets always
+    ("g7", 700, 120, 100, None, None, None, None),
+    ("g32", 300, 60, 50, None, None, None, None),
+    ("g21", 400, 60, 50, None, None, None, None),
+    ("g20", 256, 12, 1, "64", None, None, None),       # every env at once through the cooperative path
+    ("g64", 128, 12, 1, "0", None, None, None),        # every env at once through the lane-per-env path
+    ("g20", 256, 12, 1, "8", "0", None, None),         # no prefetch: in-kernel map generation
+    ("g20", 1024, 80, 60, None, "1", None, None),      # prefetch launch after every step
+    ("g20", 1024, 80, 60, None, "7", None, None),
+    ("g32", 300, 60, 50, None, "0", None, None),
+    ("g20", 1024, 80, 60, None, "5", 30, None),        # new seed mid-run: prefetched maps dropped
+    ("g64", 192, 40, 30, None, "3", 15, None),
+    ("g20", 1024, 80, 60, None, "16", None, 33),  # reset() of every env mid-run (prefetch refill)
+    ("g64", 192, 40, 30, None, None, None, 17),
 ])
-def test_desync_autoreset_parity(name, n, steps, spread, coop_max, every, reseed_at, monkeypatch):
+def test_desync_autoreset_parity(name, n, steps, spread, coop_max, every, reseed_at, reset_at, monkeypatch):
     """every: PE_PREFETCH_EVERY (steps between prefetch launches; "0" = off)."""
     from plantos_amd import PlantOSBatch
     if coop_max is not None:
@@ -77,6 +79,18 @@ def test_desync_autoreset_parity(name, n, steps, spread, coop_max, every, reseed
         if t == reseed_at:  # map stream of every later reset keyed by the new seed
             seed = 977
             b.seed(seed, reset_episode_counters=False)
+        if t == reset_at:  # reset() of every env: new maps, then the next ones prefetched again
+            r_obs = np_(b.reset()).copy()
+            for k in range(n):
+                ov.b.reset_philox(k, seed, k, int(ov.b.scal[k, O.S_EPISODE]))
+                ov.ret[k] = 0.0
+            assert (r_obs == ov.b.obs()).all()
+            # desynchronize again, so that the refilled records are consumed in the window
+            st2 = (999 - rng.integers(0, steps - t - 3, n)).astype(np.int32)
+            sc = np_(b.get_state()["scalars"])
+            sc[:, O.S_STEP] = st2
+            b.set_state(scalars=sc)
+            ov.b.scal[:, O.S_STEP] = st2
         b.synth_actions(aseed, t, out=act)
         a_np = np_(act)
         obs, rew, te, tr = b.step(act)
