@@ -782,7 +782,7 @@ __device__ __forceinline__ void quad_done_obs(const void* ka, int tile_off, int 
 }
 
 template <int C, int R, bool ONEWORD, int NW>
-__global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 1) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : (ONEWORD ? 1 : 4)) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs; multi-word NW=4: <= 128 VGPRs (4 workgroups per CU: G=25 13.1 -> 10.5 us)
   constexpr int NR = 2 * R + 3, NV = 7, EPB = kQuadEnvs, CW = NW - 1;  // CW: commit wave
   static_assert(C % NW == 0, "rays must split evenly over the waves");
   static_assert(ONEWORD || R <= 14, "funnel-shifted window row must hold 2R+5 cells");

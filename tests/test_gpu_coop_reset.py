@@ -21,6 +21,7 @@ CFG = {
     "g7": (7, 3, 3, 3, 12),
     "g32": (32, 20, 30, 9, 24),
     "g21": (21, 8, 50, 2, 10),
+    "g25": (25, 10, 12, 6, 16),   # the multi-word C16 sector kernel (train_mcts's grid)
 }
 
 
@@ -43,6 +44,7 @@ def info_rows(b, idx):
     ("g7", 700, 120, 100, None, None, None, None),
     ("g32", 300, 60, 50, None, None, None, None),
     ("g21", 400, 60, 50, None, None, None, None),
+    ("g25", 600, 80, 60, None, None, None, None),
     ("g20", 256, 12, 1, "64", None, None, None),       # every env at once through the cooperative path
     ("g64", 128, 12, 1, "0", None, None, None),        # every env at once through the lane-per-env path
     ("g20", 256, 12, 1, "8", "0", None, None),         # no prefetch: in-kernel map generation
