@@ -92,12 +92,12 @@ def cpu_model():
 
 def measured_traffic(cfg):
     """Per-launch HBM bytes of this kernel/config from the committed rocprofv3 PMC
-    summaries (profiles/pmc_*.json, tools/pmc_summary.py): FETCH_SIZE + WRITE_SIZE
+    summaries (profiles/pmc_*.json, pmc64_*.json; tools/pmc_summary.py): FETCH_SIZE + WRITE_SIZE
     in bytes, collected in separate passes.  PMC cannot run inside the timed
     process, so the bench line cites the profile it took the number from."""
     import glob
     best = None
-    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json"))):
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc*_*.json"))):  # pmc_*, pmc64_*
         try:
             d = json.load(open(p))
         except (OSError, ValueError):
