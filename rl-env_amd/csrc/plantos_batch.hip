@@ -1150,8 +1150,14 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : (ONEWORD ? 1 : 4)) void pe_s
   // stores are still in flight (no fence at the barrier above), and the compiler
   // would make every iteration of its store loop wait for them (s_waitcnt vmcnt(0)
   // before re-using a store's data registers)
-  if constexpr (!(kAblate & 1))
-    if (wv != CW) store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D, (int)threadIdx.x, 64 * (NW - 1));
+  if constexpr (!(kAblate & 1)) {
+    if constexpr (C >= 64) {  // long rows: the commit wave's share pays for its wait (64x64: 33.2 -> 32.7 us)
+      if (wv == CW) __builtin_amdgcn_s_waitcnt(0x0F70);  // tracked vmcnt(0): no wait inside the loop
+      store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D);
+    } else {
+      if (wv != CW) store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D, (int)threadIdx.x, 64 * (NW - 1));
+    }
+  }
   if (any_done && a.autoreset && !quad_coop(a, ndone) && reset_scratch_bytes(g.G, g.WPR, rl.P) <= 4 * g.D) {
     // the tile store above wrote scratch bytes into the done rows: drain it, then
     // overwrite those rows with the fresh obs built from the LDS grid image
