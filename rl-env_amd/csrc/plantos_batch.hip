@@ -999,6 +999,11 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : (ONEWORD ? 1 : 4)) void pe_s
   PE_STAMP(3);
 
   // ---- transition from LDS (every wave; wave 0 commits)
+  // the commit wave is the block's laggard through this phase (its state stores come
+  // on top of its sector): issue priority until the done barrier (same-box A/B: 9.73
+  // -> 9.65 us synchronized, 12.88 -> 12.43 us desynchronized; for the whole kernel
+  // it slowed the synchronized step)
+  if (wv == CW) __builtin_amdgcn_s_setprio(2);
   s.step = s.step < 65535 ? s.step + 1 : 65535;                  // :162
   bool ok = false, watered = false, wet_hyd = false;
   uint32_t n = 0u;
@@ -1130,6 +1135,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : (ONEWORD ? 1 : 4)) void pe_s
   // fence: __syncthreads() would make the commit wave wait for its state stores to
   // land first (s_waitcnt vmcnt(0)), although nothing in this launch reads them
   // back -- the reset path orders its own accesses (see quad_done_path).
+  if (wv == CW) __builtin_amdgcn_s_setprio(0);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   const uint64_t dmask = reinterpret_cast<const uint64_t*>(smem)[35];  // after the asm barrier ("memory")
   const uint64_t dmu = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)dmask) |
