@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PE_ABI_VERSION 2
+#define PE_ABI_VERSION 3
 
 enum pe_status {
     PE_OK = 0,
@@ -90,7 +90,14 @@ typedef struct pe_config {
     int32_t map_generation_algo; /* PE_MAP_ORIGINAL (0, plantos_env.py:338-372) or
                                     PE_MAP_MAZE (the fork's map_generation_algo='maze',
                                     gradio-app/plantos_env_new.py:355-358, 408-604; G >= 7) */
-    int32_t reserved[6];
+    /* Auto-reset tuning (speed only: every setting gives the same results).  -1 = the
+     * library's choice for the geometry (pe_default_config sets -1).              */
+    int32_t coop_max_done;      /* a step-kernel block resets up to this many done envs
+                                   wave-cooperatively, more one lane per env; 0 = always
+                                   one lane per env                                 */
+    int32_t prefetch_every;     /* steps between the launches that generate next-episode
+                                   maps ahead of time; 0 = no prefetched resets       */
+    int32_t reserved[4];
 } pe_config;
 
 enum pe_map_algo { PE_MAP_ORIGINAL = 0, PE_MAP_MAZE = 1 };
@@ -109,8 +116,9 @@ int32_t pe_obs_dim(const pe_config* c);
 int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** out);
 int pe_destroy(pe_handle* h);
 
-/* Re-key the device RNG (and optionally zero the episode counters). */
-int pe_seed(pe_handle* h, uint64_t seed, int32_t reset_episode_counters);
+/* Re-key the device RNG (and optionally zero the episode counters), ordered on
+ * `stream` after the work already queued there (step / prefetch kernels). */
+int pe_seed(pe_handle* h, uint64_t seed, int32_t reset_episode_counters, void* stream);
 
 /* Reset the envs whose mask byte is non-zero (all envs when mask == NULL) with the
  * device-rng map generator, then write obs[n_envs, D] for ALL envs (reset ones get
@@ -158,17 +166,26 @@ int pe_synth_actions(pe_handle* h, uint64_t seed, uint32_t t, int32_t* actions, 
  * layout); synchronizes the stream. */
 int pe_poll_errors(pe_handle* h, int32_t* bits, void* stream);
 
-/* Batched CurriculumWrapper (A2C_training.py:37-109), applied inside pe_step and
- * every reset path: terminated is also reported when exploration_percentage >=
- * the env's threshold (maze completed); at reset the threshold rises by the
+/* Batched CurriculumWrapper, applied inside pe_step and every reset path.  The
+ * reference has two variants of the class, selected by terminate_on_threshold:
+ *   1  A2C_training.py:37-109 (defaults 40 / 100 / +10, 3 episodes per maze):
+ *      terminated is also reported when exploration_percentage >= the env's
+ *      threshold (:101-103);
+ *   0  trainingCode.py:24-98 (defaults 30 / 100 / +5, 50 episodes per maze, the
+ *      wrapper of its DQN / RecurrentPPO trainers): reaching the threshold only
+ *      marks the maze completed (:87-89); the episode runs on until the env itself
+ *      terminates or truncates.
+ * Both: exploration_percentage >= threshold marks the maze completed; at reset the threshold rises by the
  * increment after a completed maze (capped), a new map starts after a completed
  * maze or max_episodes_per_maze episodes, and otherwise the new episode keeps the
  * previous episode's visit counts (explored map restarted; the reset obs shows the
  * fresh visits, as the wrapper installs them after env.reset()).  The reference's
  * "same maze" intent is not realized there either (reset seeds are ignored).
- * Enabling (re)initializes every env's record: threshold = initial, counters 0. */
+ * Enabling (re)initializes every env's record (threshold = initial, counters 0),
+ * ordered on `stream`. */
 int pe_curriculum_enable(pe_handle* h, double initial_threshold, double max_threshold,
-                         double threshold_increment, int32_t max_episodes_per_maze);
+                         double threshold_increment, int32_t max_episodes_per_maze,
+                         int32_t terminate_on_threshold, void* stream);
 int pe_curriculum_disable(pe_handle* h);
 /* threshold f64[n]; counters i32[n,4] = episode_count, successful_explorations,
  * episodes_on_current_maze, flags (bit0 maze_completed, bit1 visits carried). Device. */

@@ -109,18 +109,22 @@ struct Rules {
   uint32_t env_off;
   int P, O, max_steps;
   double cur_max, cur_inc;  // CurriculumWrapper max_threshold, threshold_increment
-  int cur_max_eps;          // max_episodes_per_maze (A2C_training.py:54)
+  int cur_max_eps;          // max_episodes_per_maze (A2C_training.py:54, trainingCode.py:42)
+  int cur_term;             // 1: the threshold also terminates (A2C_training.py:101-103);
+                            // 0: it only marks the maze completed (trainingCode.py:87-89)
   int map_algo;             // PE_MAP_ORIGINAL / PE_MAP_MAZE (the fork, plantos_env_new.py:355-358)
 };
 
-// CurriculumWrapper.step (A2C_training.py:97-109): exploration_percentage >= the
-// env's threshold marks the maze completed and reports terminated (the env's own
-// termination and completion bonus are untouched).  pct as the reference computes it.
-__device__ __forceinline__ bool curriculum_hit(CurRec* cur, int64_t e, double thr, int expl, int total) {
+// CurriculumWrapper.step (A2C_training.py:97-109, trainingCode.py:84-96):
+// exploration_percentage >= the env's threshold marks the maze completed and, in the
+// A2C variant (term_on_hit), reports terminated; the env's own termination and
+// completion bonus are untouched.  pct as the reference computes it.
+__device__ __forceinline__ bool curriculum_hit(CurRec* cur, int64_t e, double thr, int expl, int total,
+                                               int term_on_hit) {
   const double pct = ((double)expl / (double)total) * 100.0;  // plantos_env.py:331
   if (pct >= thr) {
     cur[e].flags |= CUR_COMPLETED;
-    return true;
+    return term_on_hit != 0;
   }
   return false;
 }

@@ -16,13 +16,14 @@ struct pe_handle {
   int variant;
   const char* kname;
   void* cur_mem;     // CurriculumWrapper records (pe_curriculum_enable), or NULL
-  size_t lds_floor;  // PE_LDS_FLOOR (diagnostics): minimum dynamic LDS per step workgroup
-  int quad_waves;    // waves per workgroup of the sector kernel (4 or 8; PE_QUAD_WAVES)
-  int stagger;       // PE_STAGGER (experimental): sector-kernel start delay per block quarter
-  int coop_max_done; // wave-cooperative auto-resets up to this many done envs per block (pe_coop.hpp)
+  size_t lds_floor;  // minimum dynamic LDS per step workgroup (PE_LDS_FLOOR, debug builds only)
+  int quad_waves;    // waves per workgroup of the sector kernel (4; 8 via PE_QUAD_WAVES in debug builds)
+  int stagger;       // sector-kernel start delay per block quarter (PE_STAGGER, debug builds only)
+  int coop_max_done; // wave-cooperative auto-resets up to this many done envs per block (pe_coop.hpp;
+                     // pe_config.coop_max_done)
   pe::Prefetch pf;   // prefetched resets (pf.scal == NULL: off)
   void* pf_mem;
-  int pf_every;      // steps between queue-mode prefetch launches (PE_PREFETCH_EVERY)
+  int pf_every;      // steps between queue-mode prefetch launches (pe_config.prefetch_every)
   int pf_count;      // steps since the last one
   int pf_blocks;     // queue-mode prefetch grid: workgroups resident at once
 };

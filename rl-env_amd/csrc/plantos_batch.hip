@@ -282,7 +282,7 @@ __global__ __launch_bounds__(kBlock) void pe_step_kernel(StepArgs a) {
     Scal s = unpack(a.st.scal[e]);
     bool term = false, trunc = false;
     double rew = transition(a, e, s, action, term, trunc);
-    if (a.st.cur) term = curriculum_hit(a.st.cur, e, a.st.cur[e].thr, s.expl, s.total) || term;
+    if (a.st.cur) term = curriculum_hit(a.st.cur, e, a.st.cur[e].thr, s.expl, s.total, a.rl.cur_term) || term;
     double ret = a.st.ep_ret[e] + rew;
     a.reward[e] = (float)rew;
     a.term[e] = term;
@@ -455,7 +455,7 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
       s.flags |= F_BONUS;
     }
     ret += rew;
-    if (st.cur) term = curriculum_hit(st.cur, e, st.cur[e].thr, s.expl, s.total) || term;
+    if (st.cur) term = curriculum_hit(st.cur, e, st.cur[e].thr, s.expl, s.total, rl.cur_term) || term;
     a.reward[e] = (float)rew;
     a.term[e] = term;
     a.trunc[e] = trunc;
@@ -1086,7 +1086,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : (ONEWORD ? 1 : 4)) void pe_s
         rew += rl.r_complete;
         s.flags |= F_BONUS;
       }
-      if (st.cur) term = curriculum_hit(st.cur, e, cthr, s.expl, s.total) || term;  // A2C_training.py:101-103
+      if (st.cur) term = curriculum_hit(st.cur, e, cthr, s.expl, s.total, rl.cur_term) || term;  // A2C_training.py:101-103
       done = term || trunc;  // terminal outputs; the reset itself only with autoreset
       // an env about to be auto-reset gets new grid and visit rows: its last move /
       // watering is not stored (the terminal info accounts for the watering), so no
@@ -1481,6 +1481,17 @@ __global__ void pe_set_env_kernel(StepArgs a, const uint8_t* cells, const int32_
   a.st.scal[e] = pack(s);
 }
 
+// CurriculumWrapper.__init__ state of every env (A2C_training.py:41-54).
+__global__ void pe_cur_init_kernel(CurRec* cur, int n, double thr) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  CurRec c;
+  c.thr = thr;
+  c.episodes = c.successes = c.on_maze = c.flags = 0u;
+  c.pad[0] = c.pad[1] = 0u;
+  cur[e] = c;
+}
+
 __global__ void pe_synth_kernel(int n, uint64_t seed, uint32_t env_off, uint32_t t, int32_t* actions) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
@@ -1686,6 +1697,8 @@ void pe_default_config(pe_config* c, int32_t G, int32_t P, int32_t O, int32_t R,
   c->r_complete = 50;
   c->seed = 0;
   c->env_id_offset = 0;
+  c->coop_max_done = -1;           // the library's choice per geometry
+  c->prefetch_every = -1;
 }
 
 int32_t pe_obs_dim(const pe_config* c) { return c->lidar_channels * 5 + 2 + 25; }
@@ -1815,29 +1828,33 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   h->variant = V_GENERIC;
   if (C == 16 && R == 6 && table_matches<16, 6>(ldx, ldy)) h->variant = g.WPR == 1 ? V_C16R6_1W : V_C16R6;
   if (C == 64 && R == 6 && table_matches<64, 6>(ldx, ldy)) h->variant = V_C64R6;
-  const char* kenv = std::getenv("PE_STEP_KERNEL");  // "lane": one-lane-per-env kernels (A/B)
-  const bool lane_kernels = kenv && std::strcmp(kenv, "lane") == 0;
+  // A/B knobs of the measurement tools (tools/ab_build.sh builds a SEPARATE library
+  // with -DPE_DEBUG_KNOBS); the product library reads no environment variable.
+  bool lane_kernels = false;
+  h->quad_waves = 4;  // measured best at C=16 and C=64 (profiles/r1c-r1e)
+  h->stagger = 0;
+  h->lds_floor = 0;
+#ifdef PE_DEBUG_KNOBS
+  if (const char* kenv = std::getenv("PE_STEP_KERNEL")) lane_kernels = std::strcmp(kenv, "lane") == 0;
+  if (const char* qw = std::getenv("PE_QUAD_WAVES")) h->quad_waves = std::atoi(qw) == 8 ? 8 : 4;
+  if (const char* sg = std::getenv("PE_STAGGER")) h->stagger = std::atoi(sg);
+  if (const char* lf = std::getenv("PE_LDS_FLOOR")) h->lds_floor = std::min<size_t>(std::strtoul(lf, nullptr, 10), 160 * 1024);
+#endif
   if (!lane_kernels && h->variant != V_GENERIC) h->variant += V_QUAD_C16R6_1W - V_C16R6_1W;
   if (is_quad(h->variant) && quad_lds_bytes(g) > 160 * 1024) h->variant -= V_QUAD_C16R6_1W - V_C16R6_1W;
   if (h->variant == V_QUAD_C16R6_1W && g.NW != 4) h->variant = V_C16R6_1W;  // needs 16-B visit rows
   h->kname = variant_name(h->variant);
+  // explicit reset-path tuning (pe_config.coop_max_done; -1: the choice above) --
+  // applied before the prefetch decision, which depends on it
+  if (c->coop_max_done >= 0 && coop_reset_ok(G, R, g.WPR, g.NW, P, C, c->map_generation_algo))
+    h->coop_max_done = std::min(c->coop_max_done, kQuadEnvs);
   // Prefetched resets (pe_coop.hpp Prefetch) where the sector kernel takes the
   // cooperative path.  The done-count threshold above stays: a whole block done at
   // once (a synchronized batch truncating) is cheaper through the lane-per-env path,
   // which consumes no record and so queues no regeneration (20x20: 0.26 ms per
   // batch reset, against 0.09 ms for the copies + ~0.3 ms to regenerate 65536 maps).
-  const char* pfe = std::getenv("PE_PREFETCH_EVERY");
-  h->pf_every = pfe ? std::atoi(pfe) : kPrefetchEvery;
+  h->pf_every = c->prefetch_every >= 0 ? c->prefetch_every : kPrefetchEvery;
   if (!is_quad(h->variant) || h->coop_max_done <= 0 || !c->autoreset) h->pf_every = 0;
-  if (const char* cm = std::getenv("PE_COOP_MAX_DONE")) h->coop_max_done = std::atoi(cm);  // A/B
-  const char* qw = std::getenv("PE_QUAD_WAVES");
-  // measured (profiles/r1c-r1e): 4 waves win at C=16, 8 waves at C=64
-  h->quad_waves = qw ? (std::atoi(qw) == 8 ? 8 : 4) : 4;  // 4 measured best at C=16 and C=64
-  const char* sg = std::getenv("PE_STAGGER");
-  h->stagger = sg ? std::atoi(sg) : 0;
-  const char* lf = std::getenv("PE_LDS_FLOOR");
-  h->lds_floor = lf ? (size_t)std::strtoul(lf, nullptr, 10) : 0;
-  if (h->lds_floor > 160 * 1024) h->lds_floor = 160 * 1024;
 
   // one device allocation carved into 256-B aligned arrays
   const size_t n = (size_t)n_envs;
@@ -1952,7 +1969,7 @@ int pe_destroy(pe_handle* h) {
 }
 
 int pe_curriculum_enable(pe_handle* h, double initial_threshold, double max_threshold, double threshold_increment,
-                         int32_t max_episodes_per_maze) {
+                         int32_t max_episodes_per_maze, int32_t terminate_on_threshold, void* stream) {
   if (!h) return fail(PE_ERR_ARG, "null handle");
   if (max_episodes_per_maze < 1) return fail(PE_ERR_ARG, "max_episodes_per_maze must be >= 1");
   DeviceGuard dg(h);
@@ -1964,15 +1981,16 @@ int pe_curriculum_enable(pe_handle* h, double initial_threshold, double max_thre
       return fail(PE_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(me));
     }
   }
-  CurRec init;
-  std::memset(&init, 0, sizeof(init));
-  init.thr = initial_threshold;  // A2C_training.py:41-54: counters 0, maze_completed False, persistent None
-  std::vector<CurRec> host((size_t)h->n, init);
-  PE_HIP(hipMemcpy(h->cur_mem, host.data(), sizeof(CurRec) * host.size(), hipMemcpyHostToDevice));
+  // A2C_training.py:41-54 / trainingCode.py:29-42: counters 0, maze_completed False,
+  // persistent None -- written on the caller's stream, after its queued steps
+  hipLaunchKernelGGL(pe_cur_init_kernel, dim3((h->n + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<CurRec*>(h->cur_mem), h->n, initial_threshold);
+  PE_HIP(hipGetLastError());
   h->st.cur = static_cast<CurRec*>(h->cur_mem);
   h->rl.cur_max = max_threshold;
   h->rl.cur_inc = threshold_increment;
   h->rl.cur_max_eps = max_episodes_per_maze;
+  h->rl.cur_term = terminate_on_threshold ? 1 : 0;
   return PE_OK;
 }
 
@@ -1997,17 +2015,21 @@ int pe_curriculum_get(pe_handle* h, double* threshold, int32_t* counters, void* 
   return PE_OK;
 }
 
-int pe_seed(pe_handle* h, uint64_t seed, int32_t reset_episode_counters) {
+int pe_seed(pe_handle* h, uint64_t seed, int32_t reset_episode_counters, void* stream) {
   if (!h) return fail(PE_ERR_ARG, "null handle");
   DeviceGuard dg(h);
   if (dg.rc) return dg.rc;
+  // on the caller's stream: a step or prefetch kernel queued before this call must
+  // finish before the records and counters are cleared (a prefetch still running
+  // could otherwise publish an old-seed record after the clear)
+  hipStream_t s = static_cast<hipStream_t>(stream);
   if (h->pf.scal && seed != h->rl.seed)  // every prefetched map belongs to the old seed
-    PE_HIP(hipMemset(h->pf.scal, 0, sizeof(uint4) * (size_t)h->n));
+    PE_HIP(hipMemsetAsync(h->pf.scal, 0, sizeof(uint4) * (size_t)h->n, s));
   h->rl.seed = seed;
   h->cfg.seed = seed;
   if (reset_episode_counters) {
     // the episode counter is the 4th word of each packed scalar record
-    PE_HIP(hipMemset2D(reinterpret_cast<char*>(h->st.scal) + 12, sizeof(uint4), 0, 4, (size_t)h->n));
+    PE_HIP(hipMemset2DAsync(reinterpret_cast<char*>(h->st.scal) + 12, sizeof(uint4), 0, 4, (size_t)h->n, s));
   }
   return PE_OK;
 }

@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(HERE, "libplantos_hip.so")
 if os.environ.get("PLANTOS_HIP_LIB"):
     LIB_PATH = os.environ["PLANTOS_HIP_LIB"]
 
-PE_ABI_VERSION = 2
+PE_ABI_VERSION = 3
 PE_OK, PE_ERR_ARG, PE_ERR_DEVICE, PE_ERR_NOMEM, PE_ERR_NOROOM = 0, -1, -2, -3, -4
 PE_NSCAL = 8
 PE_NINFO = 11
@@ -52,7 +52,8 @@ class PEConfig(ctypes.Structure):
         ("r_water_empty", ctypes.c_double), ("r_step", ctypes.c_double), ("r_exploration", ctypes.c_double),
         ("r_revisit", ctypes.c_double), ("r_complete", ctypes.c_double), ("seed", ctypes.c_uint64),
         ("env_id_offset", ctypes.c_uint32), ("map_generation_algo", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 6),
+        ("coop_max_done", ctypes.c_int32), ("prefetch_every", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 4),
     ]
 
 
@@ -81,7 +82,7 @@ def lib():
     L.pe_obs_dim.restype = I32
     L.pe_create.argtypes = [CP, I32, I32, ctypes.POINTER(P)]
     L.pe_destroy.argtypes = [P]
-    L.pe_seed.argtypes = [P, U64, I32]
+    L.pe_seed.argtypes = [P, U64, I32, P]
     L.pe_reset.argtypes = [P, P, P, P]
     L.pe_step.argtypes = [P, P, I32, P, P, P, P, P, P, P, P, P]
     L.pe_get_info.argtypes = [P, P, P]
@@ -101,7 +102,7 @@ def lib():
     L.pe_last_error.argtypes = []
     L.pe_last_error.restype = ctypes.c_char_p
     D = ctypes.c_double
-    L.pe_curriculum_enable.argtypes = [P, D, D, D, I32]
+    L.pe_curriculum_enable.argtypes = [P, D, D, D, I32, I32, P]
     L.pe_curriculum_disable.argtypes = [P]
     L.pe_curriculum_get.argtypes = [P, P, P, P]
     L.pe_pystream_create.argtypes = [CP, ctypes.c_int64, ctypes.POINTER(P)]

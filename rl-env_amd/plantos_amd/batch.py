@@ -21,11 +21,14 @@ class PlantOSBatch:
     size, device, the device-rng seed, and `env_id_offset` (global id of env 0,
     used when the batch is one shard of a multi-GPU job); `map_generation_algo`
     is the fork's ('original' or 'maze', gradio-app/plantos_env_new.py:28).
+    `coop_max_done` / `prefetch_every` tune the auto-reset paths (pe_config; None =
+    the library's choice); they change speed, never results.
     """
 
     def __init__(self, num_envs, grid_size=21, num_plants=8, num_obstacles=50, lidar_range=2,
                  lidar_channels=10, thirsty_plant_prob=0.7, max_steps=1000, autoreset=True, seed=0,
-                 env_id_offset=0, device=None, rewards=None, map_generation_algo="original"):
+                 env_id_offset=0, device=None, rewards=None, map_generation_algo="original",
+                 coop_max_done=None, prefetch_every=None):
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device() if torch.cuda.is_available() else 0)
         self.device = torch.device(device)
@@ -39,6 +42,10 @@ class PlantOSBatch:
         cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         cfg.env_id_offset = int(env_id_offset)
         cfg.map_generation_algo = C.map_algo_id(map_generation_algo)
+        if coop_max_done is not None:
+            cfg.coop_max_done = int(coop_max_done)
+        if prefetch_every is not None:
+            cfg.prefetch_every = int(prefetch_every)
         self.map_generation_algo = "maze" if cfg.map_generation_algo == C.PE_MAP_MAZE else "original"
         for k, v in (rewards or {}).items():
             setattr(cfg, k, float(v))
@@ -52,13 +59,13 @@ class PlantOSBatch:
                     "pe_create")
         self._h = h
         n, D, dev = self.num_envs, self.obs_dim, self.device
-        self.obs = torch.zeros((n, D), dtype=torch.float32, device=dev)
-        # reward f32 | terminated u8 | truncated u8 in ONE device buffer: a host-side
-        # consumer fetches the per-step scalars with a single device->host copy
-        self._packed = torch.zeros(6 * n, dtype=torch.uint8, device=dev)
-        self.reward = self._packed[:4 * n].view(torch.float32)
-        self.terminated = self._packed[4 * n:5 * n]
-        self.truncated = self._packed[5 * n:]
+        # one step's outputs in ONE device buffer (io): obs f32 [n, D] | reward f32 [n] |
+        # terminated u8 [n] | truncated u8 [n].  A host-side consumer fetches the
+        # per-step scalars with one copy, and a multi-GPU job gathers a whole step
+        # with one collective (shard.py).
+        self._io = self.new_io()
+        self.obs, self.reward, self.terminated, self.truncated = self.io_views(self._io)
+        self._packed = self._io[4 * n * D:]
         self.terminal_obs = torch.zeros((n, D), dtype=torch.float32, device=dev)
         self.episode_return = torch.zeros(n, dtype=torch.float64, device=dev)
         self.episode_length = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -90,6 +97,24 @@ class PlantOSBatch:
         if not self._h:
             raise ValueError("PlantOSBatch is closed")
         return self._h
+
+    @property
+    def io(self):
+        """u8 [4nD + 6n] device buffer of one step's outputs (see io_views)."""
+        return self._io
+
+    def io_bytes(self):
+        return 4 * self.num_envs * self.obs_dim + 6 * self.num_envs
+
+    def new_io(self):
+        """A fresh output buffer for step(io=...) (e.g. double buffering)."""
+        return torch.zeros(self.io_bytes(), dtype=torch.uint8, device=self.device)
+
+    def io_views(self, io):
+        """(obs f32 [n, D], reward f32 [n], terminated u8 [n], truncated u8 [n]) views of io."""
+        n, D = self.num_envs, self.obs_dim
+        return (io[:4 * n * D].view(torch.float32).view(n, D), io[4 * n * D:4 * n * (D + 1)].view(torch.float32),
+                io[4 * n * (D + 1):4 * n * (D + 1) + n], io[4 * n * (D + 1) + n:])
 
     @property
     def packed_outputs(self):
@@ -131,11 +156,21 @@ class PlantOSBatch:
             C.check(C.lib().pe_reset(self.handle, _ptr(m), _ptr(out), self._stream()), "pe_reset")
         return out
 
-    def step(self, actions, obs=None, want_terminal_obs=True):
+    def step(self, actions, obs=None, want_terminal_obs=True, io=None):
         """One step of every env. `actions`: int32/int64 tensor [n] on the device
         (other inputs are converted).  Returns device tensors
         (obs, reward, terminated, truncated).  Asynchronous on torch's current
-        stream (graph-capturable); the library binds and restores the device."""
+        stream (graph-capturable); the library binds and restores the device.
+        io: another output buffer (new_io()) to write this step's outputs to."""
+        if io is not None:
+            o, r_, te_, tr_ = self.io_views(io)
+            rc = self._L.pe_step(self.handle, self._actions_ptr(actions), self._act_bytes, o.data_ptr(),
+                                 r_.data_ptr(), te_.data_ptr(), tr_.data_ptr(),
+                                 self._tobs_ptr if want_terminal_obs else None, self._ep_ptrs[0], self._ep_ptrs[1],
+                                 self._ep_ptrs[2], torch.cuda.current_stream(self._dev_index).cuda_stream)
+            if rc:
+                C.check(rc, "pe_step")
+            return o, r_, te_, tr_
         a = actions
         if not (type(a) is torch.Tensor and a.is_cuda and a.get_device() == self._dev_index
                 and (a.dtype is torch.int32 or a.dtype is torch.int64) and a.is_contiguous()):
@@ -150,6 +185,17 @@ class PlantOSBatch:
         if rc:
             C.check(rc, "pe_step")
         return out, self.reward, self.terminated, self.truncated
+
+    def _actions_ptr(self, actions):
+        a = actions
+        if not (type(a) is torch.Tensor and a.is_cuda and a.get_device() == self._dev_index
+                and (a.dtype is torch.int32 or a.dtype is torch.int64) and a.is_contiguous()):
+            a = torch.as_tensor(a).to(device=self.device, dtype=torch.int64).contiguous()
+        if a.numel() != self.num_envs:
+            raise ValueError(f"expected {self.num_envs} actions, got {a.numel()}")
+        self._a_keep = a  # alive until the launch has read it
+        self._act_bytes = a.element_size()
+        return a.data_ptr()
 
     # ----------------------------------------------------------------- inspection
     def get_info(self):
@@ -205,13 +251,35 @@ class PlantOSBatch:
         return int(bits.value)
 
     # ----------------------------------------------------------------- curriculum
-    def enable_curriculum(self, initial_threshold=40.0, max_threshold=100.0, threshold_increment=10.0,
-                          max_episodes_per_maze=3):
-        """Batched CurriculumWrapper (A2C_training.py:37-109) on every env; the
-        defaults are the wrapper's as A2C_training.py:121 constructs it."""
-        C.check(C.lib().pe_curriculum_enable(self.handle, float(initial_threshold), float(max_threshold),
-                                             float(threshold_increment), int(max_episodes_per_maze)),
-                "pe_curriculum_enable")
+    # the reference's two CurriculumWrapper classes: constructor defaults as their
+    # make_env_wrapper builds them (A2C_training.py:41-54,121; trainingCode.py:29-42,107)
+    CURRICULUM_VARIANTS = {
+        "a2c": dict(initial_threshold=40.0, max_threshold=100.0, threshold_increment=10.0,
+                    max_episodes_per_maze=3, terminate_on_threshold=True),
+        "trainingCode": dict(initial_threshold=30.0, max_threshold=100.0, threshold_increment=5.0,
+                             max_episodes_per_maze=50, terminate_on_threshold=False),
+    }
+
+    def enable_curriculum(self, variant="a2c", **overrides):
+        """Batched CurriculumWrapper on every env.  variant="a2c": A2C_training.py:37-109
+        (reaching the threshold terminates the episode); variant="trainingCode":
+        trainingCode.py:24-98 (it only marks the maze completed).  Keyword overrides:
+        initial_threshold, max_threshold, threshold_increment, max_episodes_per_maze,
+        terminate_on_threshold."""
+        if variant not in self.CURRICULUM_VARIANTS:
+            raise ValueError(f"curriculum variant must be one of {sorted(self.CURRICULUM_VARIANTS)}")
+        kw = dict(self.CURRICULUM_VARIANTS[variant])
+        unknown = set(overrides) - set(kw)
+        if unknown:
+            raise TypeError(f"unknown curriculum arguments: {sorted(unknown)}")
+        kw.update(overrides)
+        with torch.cuda.device(self.device):
+            C.check(C.lib().pe_curriculum_enable(self.handle, float(kw["initial_threshold"]),
+                                                 float(kw["max_threshold"]), float(kw["threshold_increment"]),
+                                                 int(kw["max_episodes_per_maze"]),
+                                                 int(bool(kw["terminate_on_threshold"])), self._stream()),
+                    "pe_curriculum_enable")
+        self.curriculum_variant = variant
 
     def disable_curriculum(self):
         C.check(C.lib().pe_curriculum_disable(self.handle), "pe_curriculum_disable")
@@ -226,6 +294,7 @@ class PlantOSBatch:
         return thr, cnt
 
     def seed(self, seed, reset_episode_counters=True):
-        C.check(C.lib().pe_seed(self.handle, int(seed) & 0xFFFFFFFFFFFFFFFF, int(bool(reset_episode_counters))),
-                "pe_seed")
+        with torch.cuda.device(self.device):
+            C.check(C.lib().pe_seed(self.handle, int(seed) & 0xFFFFFFFFFFFFFFFF, int(bool(reset_episode_counters)),
+                                    self._stream()), "pe_seed")
         self.cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF

@@ -6,7 +6,8 @@ stream is keyed by the GLOBAL id, so a sharded job reproduces the single-GPU
 batch bit for bit).  Nothing is exchanged during a step.  The only collective is
 at the host boundary, when one consumer (a policy on rank 0) needs the global
 batch: ``gather_outputs`` moves (obs, reward, terminated, truncated) to the root
-(RCCL ``gather`` over xGMI on GPUs; gloo on CPU in the tests) and
+as ONE packed buffer per rank (RCCL ``gather`` over xGMI on GPUs; gloo on CPU in
+the tests; ``step_gather`` pipelines it behind the next step) and
 ``scatter_actions`` hands the root's actions back to the shards.
 """
 import torch
@@ -36,7 +37,7 @@ class ShardedPlantOS:
             dev = torch.device("cuda", torch.cuda.current_device())
             batch_factory = lambda n, **kw: PlantOSBatch(n, device=dev, **cfg, **kw)  # noqa: E731
         self.batch = batch_factory(self.n, env_id_offset=lo, seed=seed)
-        self._gbuf = None
+        self._slots = None
 
     @property
     def device(self):
@@ -45,25 +46,76 @@ class ShardedPlantOS:
     def step(self, actions_local):
         return self.batch.step(actions_local)
 
-    def _root_bufs(self, obs, rew, te, tr):
-        if self._gbuf is None:
-            mk = lambda t: [torch.empty_like(t) for _ in range(self.world)]  # noqa: E731
-            self._gbuf = (mk(obs), mk(rew), mk(te), mk(tr))
-        return self._gbuf
+    def _pack(self, outs):
+        """One step's outputs of this shard as ONE flat u8 buffer (the batch's io
+        buffer itself when it has one: no copy)."""
+        io = getattr(self.batch, "io", None)
+        if io is not None:
+            return io
+        return torch.cat([t.contiguous().view(-1).view(torch.uint8) for t in outs])
+
+    def _unpack(self, flats, like):
+        """Concatenate the W ranks' flat buffers into global (obs, reward, term, trunc)."""
+        n = self.n
+        D = like[0].shape[1]
+        sizes = (4 * n * D, 4 * n, n, n)
+        parts = [[], [], [], []]
+        for f in flats:
+            off = 0
+            for k, sz in enumerate(sizes):
+                parts[k].append(f[off:off + sz])
+                off += sz
+        obs = torch.cat(parts[0]).view(torch.float32).view(-1, D)
+        return obs, torch.cat(parts[1]).view(torch.float32), torch.cat(parts[2]), torch.cat(parts[3])
 
     def gather_outputs(self, root=0):
         """(obs, reward, terminated, truncated) of all ranks, concatenated in global
-        env order on `root` (None elsewhere)."""
+        env order on `root` (None elsewhere): ONE gather of each rank's packed
+        output buffer (RCCL over xGMI on GPUs)."""
         b = self.batch
         outs = (b.obs, b.reward, b.terminated, b.truncated)
         if self.world == 1:
             return outs
-        bufs = self._root_bufs(*outs) if self.rank == root else (None, None, None, None)
-        for t, lst in zip(outs, bufs):
-            dist.gather(t, lst, dst=root, group=self.group)
+        flat = self._pack(outs)
+        lst = [torch.empty_like(flat) for _ in range(self.world)] if self.rank == root else None
+        dist.gather(flat, lst, dst=root, group=self.group)
         if self.rank != root:
             return None
-        return tuple(torch.cat(lst, 0) for lst in bufs)
+        return self._unpack(lst, outs)
+
+    def step_gather(self, actions_local, root=0):
+        """Pipelined step + host-boundary gather (GPU batches): the step writes into
+        one of two output buffers and its gather to `root` is issued asynchronously,
+        so the gather of step t overlaps step t+1; before a buffer is written again
+        the stream waits for its previous gather.  Returns the slot used; the
+        gathered buffers of a slot are `gathered(slot)` on root once `flush()` (or
+        the slot's next use) has waited for it."""
+        b = self.batch
+        if self._slots is None:
+            self._slots = [b.new_io(), b.new_io()]
+            self._glist = [[torch.empty_like(self._slots[k]) for _ in range(self.world)] if self.rank == root
+                           else None for k in range(2)]
+            self._work = [None, None]
+            self._k = 0
+        k = self._k
+        self._k ^= 1
+        if self._work[k] is not None:
+            self._work[k].wait()  # the stream waits for the slot's previous gather
+        b.step(actions_local, io=self._slots[k])
+        if self.world > 1:
+            self._work[k] = dist.gather(self._slots[k], self._glist[k], dst=root, group=self.group, async_op=True)
+        return k
+
+    def gathered(self, k):
+        return self._glist[k]
+
+    def flush(self):
+        if self._slots is None:
+            return
+        for k in range(2):
+            if self._work[k] is not None:
+                self._work[k].wait()
+                self._work[k] = None
 
     def scatter_actions(self, actions_global=None, root=0):
         """Root's global action vector -> this rank's shard (int64 [n])."""

@@ -235,9 +235,13 @@ class PlantOSVecEnv(_VecEnvBase):
         episode) -- the throughput mode.  reset_mode="cpython": the reference's own
         layouts, seed-exact: CPython's global `random` after random.seed(python_seed)
         (default: seed), consumed in DummyVecEnv order (pe_pystream, host side).
-        curriculum=True (or a dict of CurriculumWrapper arguments) applies the batched
-        CurriculumWrapper of A2C_training.py:37-109 to every env, as
-        make_env_wrapper(use_curriculum=True) does (A2C_training.py:114-126).
+        curriculum=True (or "a2c") applies the batched CurriculumWrapper of
+        A2C_training.py:37-109 to every env, as make_env_wrapper(use_curriculum=True)
+        does (A2C_training.py:114-126); curriculum="trainingCode" the variant of
+        trainingCode.py:24-98 (threshold marks the maze completed without
+        terminating; 30 / 100 / +5, 50 episodes per maze) as its make_env_wrapper
+        does (trainingCode.py:103-111); a dict {"variant": ..., **CurriculumWrapper
+        arguments} overrides the defaults.
         map_generation_algo="maze" selects the fork's maze layouts
         (gradio-app/plantos_env_new.py:28, 408-604) in either reset mode.
         host_buffers=k (numpy face): obs arrive in a ring of k pinned host buffers
@@ -255,10 +259,11 @@ class PlantOSVecEnv(_VecEnvBase):
             max_steps=max_steps, autoreset=reset_mode == "device", seed=seed, env_id_offset=env_id_offset,
             device=device, map_generation_algo=map_generation_algo)
         if curriculum:
-            kw = dict(initial_threshold=40.0, max_threshold=100.0)  # A2C_training.py:121
-            if isinstance(curriculum, dict):
-                kw.update(curriculum)
-            self.batch.enable_curriculum(**kw)
+            # True / "a2c": A2C_training.py:37-109 as :121 builds it; "trainingCode":
+            # trainingCode.py:24-98 as :107 builds it; a dict: {"variant": ..., overrides}
+            kw = dict(curriculum) if isinstance(curriculum, dict) else {}
+            variant = curriculum if isinstance(curriculum, str) else kw.pop("variant", "a2c")
+            self.batch.enable_curriculum(variant, **kw)
         self.curriculum = bool(curriculum)
         self._pystream = None
         if reset_mode == "cpython":

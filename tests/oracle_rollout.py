@@ -85,7 +85,32 @@ class OracleBatch:
         self.obs = self.torch.as_tensor(self.ov.obs())
         return self.obs
 
-    def step(self, actions):
+    # PlantOSBatch's packed output buffer: obs f32 [n, D] | reward f32 | term u8 | trunc u8
+    def io_bytes(self):
+        return 4 * self.num_envs * self.obs_dim + 6 * self.num_envs
+
+    def new_io(self):
+        return self.torch.zeros(self.io_bytes(), dtype=self.torch.uint8)
+
+    def io_views(self, io):
+        n, D = self.num_envs, self.obs_dim
+        f32 = self.torch.float32
+        return (io[:4 * n * D].view(f32).view(n, D), io[4 * n * D:4 * n * (D + 1)].view(f32),
+                io[4 * n * (D + 1):4 * n * (D + 1) + n], io[4 * n * (D + 1) + n:])
+
+    @property
+    def io(self):
+        io = self.new_io()
+        for dst, src in zip(self.io_views(io), (self.obs, self.reward, self.terminated, self.truncated)):
+            dst.copy_(src)
+        return io
+
+    def step(self, actions, io=None):
+        if io is not None:
+            outs = self.step(actions)
+            for dst, src in zip(self.io_views(io), outs):
+                dst.copy_(src)
+            return self.io_views(io)
         a = np.asarray(actions.cpu().numpy() if hasattr(actions, "cpu") else actions, np.int64)
         pre_info = None
         obs, rew, te, tr, tobs, ret, ln = None, None, None, None, None, None, None

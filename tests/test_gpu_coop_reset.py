@@ -3,7 +3,7 @@ DESYNCHRONIZED episodes (every env starts at its own step count, so a few envs
 reset in every step, as in steady-state training): prefetched resets (maps
 generated ahead by pe_prefetch_kernel, at several launch cadences, across a seed
 change), the wave-cooperative reset (pe_coop.hpp) and, forced through
-PE_COOP_MAX_DONE / PE_PREFETCH_EVERY, every path for dense resets.  Every output of every step is
+pe_config.coop_max_done / prefetch_every, every path for dense resets.  Every output of every step is
 compared, plus the terminal info rows and the final state.
 """
 import numpy as np
@@ -56,17 +56,15 @@ def info_rows(b, idx):
     ("g20", 1024, 80, 60, None, "16", None, 33),  # reset() of every env mid-run (prefetch refill)
     ("g64", 192, 40, 30, None, None, None, 17),
 ])
-def test_desync_autoreset_parity(name, n, steps, spread, coop_max, every, reseed_at, reset_at, monkeypatch):
-    """every: PE_PREFETCH_EVERY (steps between prefetch launches; "0" = off)."""
+def test_desync_autoreset_parity(name, n, steps, spread, coop_max, every, reseed_at, reset_at):
+    """coop_max / every: pe_config.coop_max_done / prefetch_every (steps between
+    prefetch launches; "0" = off)."""
     from plantos_amd import PlantOSBatch
-    if coop_max is not None:
-        monkeypatch.setenv("PE_COOP_MAX_DONE", coop_max)
-    if every is not None:
-        monkeypatch.setenv("PE_PREFETCH_EVERY", every)
     G, P, Ob, R, C = cfg = CFG[name]
     seed = aseed = 31
     b = PlantOSBatch(n, grid_size=G, num_plants=P, num_obstacles=Ob, lidar_range=R, lidar_channels=C, seed=seed,
-                     device="cuda:0")
+                     device="cuda:0", coop_max_done=None if coop_max is None else int(coop_max),
+                     prefetch_every=None if every is None else int(every))
     ov = OracleVec(cfg, np.arange(n), seed)
     # desynchronize: env e starts at step 1000 - 1 - k(e), k in [0, spread)
     rng = np.random.default_rng(5)
@@ -129,19 +127,14 @@ def test_desync_autoreset_parity(name, n, steps, spread, coop_max, every, reseed
 def test_desync_curriculum_cooperative_reset():
     """CurriculumWrapper (visit counts carried into the next episode, explored map
     restarted) through the cooperative reset: state after sparse resets equals the
-    lane-per-env path's (PE_COOP_MAX_DONE=0) on the same inputs."""
+    lane-per-env path's (coop_max_done=0) on the same inputs."""
     from plantos_amd import PlantOSBatch
-    import os
     G, P, Ob, R, C = CFG["g20"]
     n, steps = 512, 60
     outs = []
-    for cm in ("8", "0"):
-        os.environ["PE_COOP_MAX_DONE"] = cm
-        try:
-            b = PlantOSBatch(n, grid_size=G, num_plants=P, num_obstacles=Ob, lidar_range=R, lidar_channels=C,
-                             seed=3, device="cuda:0")
-        finally:
-            del os.environ["PE_COOP_MAX_DONE"]
+    for cm in (8, 0):
+        b = PlantOSBatch(n, grid_size=G, num_plants=P, num_obstacles=Ob, lidar_range=R, lidar_channels=C,
+                         seed=3, device="cuda:0", coop_max_done=cm)
         b.enable_curriculum(initial_threshold=5.0, max_threshold=100.0)
         sc = np_(b.get_state()["scalars"])
         sc[:, O.S_STEP] = 999 - np.random.default_rng(2).integers(0, 50, n)

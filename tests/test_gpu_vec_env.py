@@ -120,10 +120,12 @@ def test_cpython_mode_reproduces_reference_dummyvecenv(name):
     v.close()
 
 
-@pytest.mark.parametrize("name", ["curriculum_g20_explore", "curriculum_g7_explore", "curriculum_g20_random"])
+@pytest.mark.parametrize("name", ["curriculum_g20_explore", "curriculum_g7_explore", "curriculum_g20_random",
+                                  "curriculum_tc_g20_explore", "curriculum_tc_g7_explore", "curriculum_tc_g20_random"])
 def test_curriculum_reproduces_reference_wrapper(name):
-    """PlantOSVecEnv(curriculum=True, reset_mode='cpython') against the reference's
-    CurriculumWrapper + env in a DummyVecEnv loop (tests/golden/curriculum_*.npz):
+    """PlantOSVecEnv(curriculum=True / "trainingCode", reset_mode='cpython') against the
+    reference's CurriculumWrapper (A2C_training.py:37-109 / trainingCode.py:24-98) + env
+    in a DummyVecEnv loop (tests/golden/curriculum_*.npz, curriculum_tc_*.npz):
     obs (incl. carried visit slices), rewards, curriculum terminations, terminal
     obs, per-step thresholds and the final wrapper counters."""
     from golden_util import cfg_tuple, load
@@ -131,7 +133,8 @@ def test_curriculum_reproduces_reference_wrapper(name):
     G, P, O, R, C = cfg_tuple(f)
     T, N = f["actions"].shape
     v = PlantOSVecEnv(N, grid_size=G, num_plants=P, num_obstacles=O, lidar_range=R, lidar_channels=C,
-                      device="cuda:0", reset_mode="cpython", python_seed=int(f["seed"]), curriculum=True)
+                      device="cuda:0", reset_mode="cpython", python_seed=int(f["seed"]),
+                      curriculum="trainingCode" if "_tc_" in name else True)
     assert (v.reset() == f["obs0"]).all()
     for t in range(T):
         obs, rew, done, infos = v.step(f["actions"][t])

@@ -1,7 +1,8 @@
 """The CurriculumWrapper restatement (test infrastructure, over the oracle) against
-the reference's own wrapper: tests/golden/curriculum_*.npz were produced by the
-reference class A2C_training.py:37-109 around the reference env (tools/gen_golden.py)
-in a DummyVecEnv loop.  Pins the semantics the device implements: threshold
+the reference's own wrappers: tests/golden/curriculum_*.npz were produced by the
+reference class A2C_training.py:37-109, curriculum_tc_*.npz by trainingCode.py:24-98
+(threshold marks the maze completed but does not terminate), around the reference
+env (tools/gen_golden.py) in a DummyVecEnv loop.  Pins the semantics the device implements: threshold
 termination, threshold increments, visit counts carried into the next episode
 with the explored map restarted, and the stale reset obs."""
 import numpy as np
@@ -14,13 +15,18 @@ from oracle import oracle as O
 class OracleCurriculumVec:
     """DummyVecEnv([CurriculumWrapper(env)]) over the oracle, CPython reset stream."""
 
-    def __init__(self, cfg, n, seed, initial=40.0, maximum=100.0, inc=10.0, max_eps=3):
+    # constructor defaults of the two reference classes as their make_env_wrapper builds them
+    VARIANTS = {"a2c": dict(initial=40.0, maximum=100.0, inc=10.0, max_eps=3, terminate=True),  # A2C_training.py:41-54
+                "tc": dict(initial=30.0, maximum=100.0, inc=5.0, max_eps=50, terminate=False)}  # trainingCode.py:29-42
+
+    def __init__(self, cfg, n, seed, initial=40.0, maximum=100.0, inc=10.0, max_eps=3, terminate=True):
         self.c = O.config(*cfg)
         self.b = O.Batch(self.c, n)
         self.mt = O.MT(seed)
         self.n = n
         self.thr = np.full(n, initial)
         self.maximum, self.inc, self.max_eps = maximum, inc, max_eps
+        self.terminate = terminate
         self.episodes = np.zeros(n, np.int64)
         self.successes = np.zeros(n, np.int64)
         self.on_maze = np.zeros(n, np.int64)
@@ -58,9 +64,10 @@ class OracleCurriculumVec:
         tobs = obs.copy()
         ex = (self.b.explored > 0).reshape(self.n, -1).sum(1).astype(np.float64)        # plantos_env.py:320
         tc = (self.b.cells != 1).reshape(self.n, -1).sum(1).astype(np.float64)           # :321
-        hit = (ex / tc) * 100 >= self.thr                                                # A2C_training.py:101
+        hit = (ex / tc) * 100 >= self.thr                                  # A2C_training.py:101, trainingCode.py:87
         self.completed |= hit
-        te |= hit
+        if self.terminate:                                                  # A2C_training.py:103 only
+            te |= hit
         for e in range(self.n):
             if self.persistent[e] is not None:
                 self.persistent[e] = self.b.visits[e].copy()
@@ -70,11 +77,14 @@ class OracleCurriculumVec:
         return obs, rew, te, tr, tobs
 
 
-@pytest.mark.parametrize("name", ["curriculum_g20_explore", "curriculum_g7_explore", "curriculum_g20_random"])
+@pytest.mark.parametrize("name", ["curriculum_g20_explore", "curriculum_g7_explore", "curriculum_g20_random",
+                                  "curriculum_tc_g20_explore", "curriculum_tc_g7_explore", "curriculum_tc_g20_random"])
 def test_curriculum_restatement_matches_reference(name):
+    """curriculum_*: A2C_training.py's wrapper; curriculum_tc_*: trainingCode.py's."""
     f = load(name)
     T, N = f["actions"].shape
-    v = OracleCurriculumVec(cfg_tuple(f), N, int(f["seed"]))
+    v = OracleCurriculumVec(cfg_tuple(f), N, int(f["seed"]),
+                            **OracleCurriculumVec.VARIANTS["tc" if "_tc_" in name else "a2c"])
     assert (v.reset() == f["obs0"]).all()
     for t in range(T):
         obs, rew, te, tr, tobs = v.step(f["actions"][t])

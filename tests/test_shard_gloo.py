@@ -21,7 +21,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, steps, q):
+def _worker(rank, world, port, n, steps, q, pipelined=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     repo = os.path.dirname(here)
@@ -51,8 +51,13 @@ def _worker(rank, world, port, n, steps, q):
             a_glob = torch.as_tensor(rng.integers(0, 5, world * n))
             a_loc = sh.scatter_actions(a_glob if rank == 0 else None)
             assert (a_loc.numpy() == a_glob.numpy()[rank * n:(rank + 1) * n]).all()
-            sh.step(a_loc)
-            g = sh.gather_outputs()
+            if pipelined:
+                k = sh.step_gather(a_loc)
+                sh.flush()
+                g = sh._unpack(sh.gathered(k), sh.batch.io_views(sh._slots[k])) if rank == 0 else None
+            else:
+                sh.step(a_loc)
+                g = sh.gather_outputs()
             if rank == 0:
                 obs, rew, te, tr, *_ = full.step(a_glob.numpy())
                 ok &= bool((g[0].numpy() == obs).all() and (g[1].numpy() == rew.astype(np.float32)).all())
@@ -65,14 +70,25 @@ def _worker(rank, world, port, n, steps, q):
         dist.destroy_process_group()
 
 
-def test_two_rank_shards_equal_one_batch():
+def _run(pipelined):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, 6, 40, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, 6, 40, q, pipelined)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=240)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=5) is True
+
+
+def test_two_rank_shards_equal_one_batch():
+    """one packed gather per step (gather_outputs)"""
+    _run(False)
+
+
+def test_pipelined_step_gather_equals_one_batch():
+    """step_gather: double-buffered outputs, each step's gather issued asynchronously
+    and waited for only before its buffer is written again (flush at the end)"""
+    _run(True)

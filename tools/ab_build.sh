@@ -14,7 +14,7 @@ else
   git -C "$ROOT" archive "$REV" rl-env_amd/csrc include | tar -x -C "$SRC"
 fi
 if [ -n "${PATCH_PY:-}" ]; then (cd "$SRC" && python3 "$PATCH_PY"); fi
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -w ${EXTRA_FLAGS:-} \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -w -DPE_DEBUG_KNOBS ${EXTRA_FLAGS:-} \
   -o "$ROOT/build/ab/lib_$NAME.so" "$SRC/rl-env_amd/csrc/plantos_batch.hip" \
   "$SRC/rl-env_amd/csrc/pe_mcts.hip" "$SRC/rl-env_amd/csrc/pe_pystream.cpp"
 echo "$ROOT/build/ab/lib_$NAME.so"

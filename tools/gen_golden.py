@@ -399,14 +399,15 @@ def gen_traj(cfg, n_envs, steps, seed, policy):
     print(f"traj_{cfg}_{policy}: {n_envs}x{steps}, resets={len(reset_maps)}, term={int(te.sum())}")
 
 
-def load_curriculum_wrapper():
-    """The reference's own CurriculumWrapper class (A2C_training.py:37-109), compiled
-    from the reference file: only that class definition is executed (the module's
-    stable_baselines3 / matplotlib imports and directory creation are skipped --
-    those packages are absent here and not part of the wrapper)."""
+def load_curriculum_wrapper(source="A2C_training.py"):
+    """The reference's own CurriculumWrapper class (A2C_training.py:37-109, or the
+    trainingCode.py:24-98 variant), compiled from the reference file: only that class
+    definition is executed (the module's stable_baselines3 / sb3_contrib / matplotlib
+    imports and directory creation are skipped -- those packages are absent here and
+    not part of the wrapper)."""
     import ast
     import gymnasium as gym_shim
-    path = os.path.join(REF, "A2C_training.py")
+    path = os.path.join(REF, source)
     tree = ast.parse(open(path).read())
     node = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "CurriculumWrapper")
     ns = {"gym": gym_shim, "np": np}
@@ -414,11 +415,17 @@ def load_curriculum_wrapper():
     return ns["CurriculumWrapper"]
 
 
-def gen_curriculum(cfg, n_envs, steps, seed, policy):
+def gen_curriculum(cfg, n_envs, steps, seed, policy, variant="a2c"):
     """DummyVecEnv over CurriculumWrapper(fork env, 40, 100) (A2C_training.py:114-126
-    with use_curriculum=True; Monitor omitted: it does not change the step data)."""
-    CW = load_curriculum_wrapper()
-    envs = [CW(make(ForkEnv, cfg), initial_threshold=40.0, max_threshold=100.0) for _ in range(n_envs)]
+    with use_curriculum=True; Monitor omitted: it does not change the step data), or
+    (variant "tc") over trainingCode.py's CurriculumWrapper(env, 30, 100) as its
+    make_env_wrapper builds it (trainingCode.py:103-111)."""
+    if variant == "tc":
+        CW = load_curriculum_wrapper("trainingCode.py")
+        envs = [CW(make(ForkEnv, cfg), initial_threshold=30.0, max_threshold=100.0) for _ in range(n_envs)]
+    else:
+        CW = load_curriculum_wrapper()
+        envs = [CW(make(ForkEnv, cfg), initial_threshold=40.0, max_threshold=100.0) for _ in range(n_envs)]
     G = envs[0].env.grid_size
     random.seed(seed)
     np.random.seed(seed + 7)  # the wrapper's np.random.randint "maze seeds" (ignored by the env)
@@ -453,12 +460,14 @@ def gen_curriculum(cfg, n_envs, steps, seed, policy):
     fin = np.array([[w.episode_count, w.successful_explorations, w.episodes_on_current_maze,
                      int(w.maze_completed) | (2 * int(w.persistent_visit_counts is not None))] for w in envs],
                    np.int32)
+    name = f"curriculum_{'tc_' if variant == 'tc' else ''}{cfg}_{policy}"
     np.savez_compressed(
-        os.path.join(OUT, f"curriculum_{cfg}_{policy}.npz"), config=np.array(CONFIGS[cfg], np.int32),
+        os.path.join(OUT, f"{name}.npz"), config=np.array(CONFIGS[cfg], np.int32),
         seed=np.int64(seed), obs0=obs0, actions=acts, obs=obs, terminal_obs=term_obs, reward=rew,
         terminated=te, truncated=tr, threshold=thr, visits_sum=visits_sum, final_counters=fin,
         next_u32=np.int64(random.getrandbits(32)))
-    print(f"curriculum_{cfg}_{policy}: {n_envs}x{steps}, term={int(te.sum())}, thr_max={thr.max()}, G={G}")
+    print(f"{name}: {n_envs}x{steps}, term={int(te.sum())}, thr_max={thr.max()}, G={G}, "
+          f"successes={fin[:, 1].tolist()}")
 
 
 def load_mcts():
@@ -645,8 +654,19 @@ def main_mcts():
     gen_mcts("g20d", "g20", 100, 50, 1, 4, 800)
 
 
+def main_curriculum_tc():
+    """trainingCode.py's CurriculumWrapper (threshold marks the maze completed
+    without terminating)."""
+    os.makedirs(OUT, exist_ok=True)
+    gen_curriculum("g20", 3, 2100, 21, "random", "tc")
+    gen_curriculum("g7", 6, 500, 22, "explore", "tc")
+    gen_curriculum("g20", 4, 1500, 23, "explore", "tc")
+
+
 if __name__ == "__main__":
-    if sys.argv[1:] == ["mcts"]:
+    if sys.argv[1:] == ["curriculum_tc"]:
+        main_curriculum_tc()
+    elif sys.argv[1:] == ["mcts"]:
         main_mcts()
     elif sys.argv[1:] == ["maze"]:
         main_maze()

@@ -14,7 +14,9 @@ dominant kernel:
   fetch_bytes_x2       = 2 * FETCH_SIZE * 1024  (gfx950: FETCH_SIZE counts half of a
                          wide coalesced streaming read; upper bound for our mix of
                          16-B coalesced and 4/8-B gathered loads)
-  traffic (reported)   = fetch_bytes_raw + write_bytes; traffic_hi adds the x2 fetch.
+  traffic             = fetch_bytes_raw + write_bytes (raw counters);
+  traffic_hi          = fetch_bytes_x2 + write_bytes: the corrected figure bench.py reports as
+                        roofline.traffic (for a profile whose lib_sha is the benched library's).
 """
 import argparse
 import collections
@@ -80,6 +82,7 @@ def main():
             b = json.loads(line)
             n = b["config"]["envs_per_gpu"]
             out["config"] = b["config"]
+            out["lib_sha"] = b.get("lib_sha")  # bench.py cites this profile only for this exact library
             out["traffic_per_env_step"] = out["traffic"] / n
             out["traffic_hi_per_env_step"] = out["traffic_hi"] / n
         except (OSError, IndexError, KeyError, ValueError):

@@ -25,7 +25,7 @@ def build(ablate=0):
     so = SO if not ablate else SO.replace(".so", f"_abl{ablate}.so")
     os.makedirs(os.path.dirname(so), exist_ok=True)
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                    "-DPE_STAMPS", f"-DPE_ABLATE={ablate}", "-o", so,
+                    "-DPE_STAMPS", "-DPE_DEBUG_KNOBS", f"-DPE_ABLATE={ablate}", "-o", so,
                     os.path.join(REPO, "rl-env_amd", "csrc", "plantos_batch.hip")], check=True)
     print(so)
 
