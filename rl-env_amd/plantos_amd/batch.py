@@ -203,17 +203,20 @@ class PlantOSBatch:
             C.check(C.lib().pe_get_info(self.handle, _ptr(self.info_buf), self._stream()), "pe_get_info")
         return self.info_buf
 
-    def get_state(self):
-        """Canonical state in the reference's terms (plantos_env.py:96-123)."""
+    def get_state(self, parts=("cells", "visits", "explored", "scalars")):
+        """Canonical state in the reference's terms (plantos_env.py:96-123); `parts`
+        selects which arrays to export (the rest are not materialized)."""
         n, G = self.num_envs, self.grid_size
-        cells = torch.empty((n, G, G), dtype=torch.uint8, device=self.device)
-        visits = torch.empty((n, G, G), dtype=torch.int32, device=self.device)
-        explored = torch.empty((n, G, G), dtype=torch.int8, device=self.device)
-        scal = torch.empty((n, C.PE_NSCAL), dtype=torch.int32, device=self.device)
+        dev = self.device
+        cells = torch.empty((n, G, G), dtype=torch.uint8, device=dev) if "cells" in parts else None
+        visits = torch.empty((n, G, G), dtype=torch.int32, device=dev) if "visits" in parts else None
+        explored = torch.empty((n, G, G), dtype=torch.int8, device=dev) if "explored" in parts else None
+        scal = torch.empty((n, C.PE_NSCAL), dtype=torch.int32, device=dev) if "scalars" in parts else None
         with torch.cuda.device(self.device):
             C.check(C.lib().pe_get_state(self.handle, _ptr(cells), _ptr(visits), _ptr(explored), _ptr(scal),
                                          self._stream()), "pe_get_state")
-        return {"cells": cells, "visits": visits, "explored": explored, "scalars": scal}
+        out = {"cells": cells, "visits": visits, "explored": explored, "scalars": scal}
+        return {k: v for k, v in out.items() if v is not None}
 
     def set_state(self, cells=None, visits=None, explored=None, scalars=None):
         def dev(x, dt):

@@ -142,7 +142,7 @@ class OracleBatch:
     def get_info(self):
         return self.torch.as_tensor(self._info_rows())
 
-    def get_state(self):
+    def get_state(self, parts=None):
         b = self.ov.b
         T = self.torch
         return {"cells": T.as_tensor(b.cells.copy()), "visits": T.as_tensor(b.visits.copy()),

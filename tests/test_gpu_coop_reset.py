@@ -38,27 +38,37 @@ def info_rows(b, idx):
     return rows
 
 
-@pytest.mark.parametrize("name,n,steps,spread,coop_max,every,reseed_at,reset_at", [
-    ("g20", 2048, 160, 150, None, None, None, None),   # sparse: prefetched / cooperative resets
-    ("g64", 192, 50, 40, None, None, None, None),      # 64x64: cooperative resets always
-    ("g7", 700, 120, 100, None, None, None, None),
-    ("g32", 300, 60, 50, None, None, None, None),
-    ("g21", 400, 60, 50, None, None, None, None),
-    ("g25", 600, 80, 60, None, None, None, None),
-    ("g20", 256, 12, 1, "64", None, None, None),       # every env at once through the cooperative path
-    ("g64", 128, 12, 1, "0", None, None, None),        # every env at once through the lane-per-env path
-    ("g20", 256, 12, 1, "8", "0", None, None),         # no prefetch: in-kernel map generation
-    ("g20", 1024, 80, 60, None, "1", None, None),      # prefetch launch after every step
-    ("g20", 1024, 80, 60, None, "7", None, None),
-    ("g32", 300, 60, 50, None, "0", None, None),
-    ("g20", 1024, 80, 60, None, "5", 30, None),        # new seed mid-run: prefetched maps dropped
-    ("g64", 192, 40, 30, None, "3", 15, None),
-    ("g20", 1024, 80, 60, None, "16", None, 33),  # reset() of every env mid-run (prefetch refill)
-    ("g64", 192, 40, 30, None, None, None, 17),
+@pytest.mark.parametrize("name,n,steps,spread,coop_max,every,reseed_at,reset_at,side", [
+    ("g20", 2048, 160, 150, None, None, None, None, False),   # sparse: prefetched / cooperative resets
+    ("g64", 192, 50, 40, None, None, None, None, False),      # 64x64: cooperative resets always
+    ("g7", 700, 120, 100, None, None, None, None, False),
+    ("g32", 300, 60, 50, None, None, None, None, False),
+    ("g21", 400, 60, 50, None, None, None, None, False),
+    ("g25", 600, 80, 60, None, None, None, None, False),
+    ("g20", 256, 12, 1, "64", None, None, None, False),       # every env at once through the cooperative path
+    ("g64", 128, 12, 1, "0", None, None, None, False),        # every env at once through the lane-per-env path
+    ("g20", 256, 12, 1, "8", "0", None, None, False),         # no prefetch: in-kernel map generation
+    ("g20", 1024, 80, 60, None, "1", None, None, False),      # prefetch launch after every step
+    ("g20", 1024, 80, 60, None, "7", None, None, False),
+    ("g32", 300, 60, 50, None, "0", None, None, False),
+    ("g20", 1024, 80, 60, None, "5", 30, None, False),        # new seed mid-run: prefetched maps dropped
+    ("g64", 192, 40, 30, None, "3", 15, None, False),
+    ("g20", 1024, 80, 60, None, "16", None, 33, False),  # reset() of every env mid-run (prefetch refill)
+    ("g64", 192, 40, 30, None, None, None, 17, False),
+    ("g20", 1024, 80, 60, None, "1", 30, None, True),  # steps + reseed on a side stream
 ])
-def test_desync_autoreset_parity(name, n, steps, spread, coop_max, every, reseed_at, reset_at):
+def test_desync_autoreset_parity(name, n, steps, spread, coop_max, every, reseed_at, reset_at, side):
     """coop_max / every: pe_config.coop_max_done / prefetch_every (steps between
-    prefetch launches; "0" = off)."""
+    prefetch launches; "0" = off).  side: everything on a non-default torch stream
+    (pe_seed must clear the prefetched records on THAT stream, after the queued
+    prefetch launches)."""
+    import contextlib
+    ctx = torch.cuda.stream(torch.cuda.Stream()) if side else contextlib.nullcontext()
+    with ctx:
+        _desync_run(name, n, steps, spread, coop_max, every, reseed_at, reset_at)
+
+
+def _desync_run(name, n, steps, spread, coop_max, every, reseed_at, reset_at):
     from plantos_amd import PlantOSBatch
     G, P, Ob, R, C = cfg = CFG[name]
     seed = aseed = 31

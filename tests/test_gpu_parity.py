@@ -169,36 +169,61 @@ def test_rollout_parity_device_rng(name, n, steps):
     b.close()
 
 
-def test_headline_size_sampled_parity_and_invariants():
-    """65536 envs (BASELINE headline) for 1100 steps: oracle replays a sample of
-    global env ids (envs are independent), plus size-independent invariants."""
-    cfg = CFG["g20"]
-    n, seed, steps = 65536, 5, 1100
+@pytest.mark.parametrize("name,desync", [("g20", False), ("g20", True), ("g64", False), ("g64", True)])
+def test_full_batch_sampled_parity_and_invariants(name, desync):
+    """65536 envs (BASELINE headline 20x20/16 rays and the 64x64/64-ray stress
+    config) for 1010+ steps, crossing the 1000-step truncation: the oracle replays
+    192 sampled global env ids (envs are independent) every step, and size-
+    independent invariants hold over ALL envs (one-hot per ray, distances in {r/R},
+    positions in {x/G}, slice values in {k/10}, episode counts and step counts
+    after the truncations).  desync: every env starts at its own step count in
+    [0, 1000) -- ~65 auto-resets in every step through the prefetched /
+    cooperative reset paths."""
+    cfg = CFG[name]
+    G, C, R = cfg[0], cfg[4], cfg[3]
+    n, seed, steps = 65536, 5, 1010 if name == "g64" else 1100
     b = make(cfg, n, seed=seed)
     sample = np.r_[0:64, 30000:30064, 65472:65536]
     ov = OracleVec(cfg, sample, seed)
+    start = np.zeros(n, np.int32)
+    if desync:
+        start = np.random.default_rng(11).integers(0, 1000, n).astype(np.int32)
+        sc = np_(b.get_state(parts=("scalars",))["scalars"])
+        sc[:, O.S_STEP] = start
+        b.set_state(scalars=sc)
+        ov.b.scal[:, O.S_STEP] = start[sample]
     act = torch.empty(n, dtype=torch.int32, device="cuda:0")
-    total_ret = torch.zeros(n, dtype=torch.float64, device="cuda:0")
+    sidx = torch.as_tensor(sample, device="cuda:0")
+    dist = np.float32(np.arange(1, R + 1) / R)
+    posv = np.float32(np.arange(G) / G)
+    visv = np.float32(np.arange(11) / 10.0)
     for t in range(steps):
         b.synth_actions(seed, t, out=act)
         obs, rew, te, tr = b.step(act)
-        o_obs, o_rew, o_te, o_tr, *_ = ov.step(np_(act)[sample])
+        o_obs, o_rew, o_te, o_tr, o_tobs, o_ret, o_len = ov.step(np_(act[sidx]))
+        assert (np_(rew[sidx]) == o_rew.astype(np.float32)).all(), t
+        assert (np_(te[sidx]).astype(bool) == o_te).all() and (np_(tr[sidx]).astype(bool) == o_tr).all(), t
+        done = o_te | o_tr
+        if done.any():
+            assert (np_(b.terminal_obs[sidx])[done] == o_tobs[done]).all(), t
+            assert (np_(b.episode_return[sidx])[done] == o_ret[done]).all(), t
+            assert (np_(b.episode_length[sidx])[done] == o_len[done]).all(), t
+        if not (t % 50 == 0 or t in (999, 1000)) and done.any():
+            assert (np_(obs[sidx]) == o_obs).all(), t  # fresh reset obs of the sampled done envs
         if t % 50 == 0 or t in (999, 1000):
             ob = np_(obs)
             assert (ob[sample] == o_obs).all(), t
-            assert (np_(rew)[sample] == o_rew.astype(np.float32)).all(), t
-            # invariants: one-hot per ray, distances in {r/R}, visit slice in {k/10}
-            lid = ob[:, :80].reshape(n, 16, 5)
-            assert (lid[:, :, 1:].sum(-1) == 1.0).all()
-            assert np.isin(lid[:, :, 0], np.float32(np.arange(1, 7) / 6.0)).all()
-            assert np.isin(ob[:, 82:], np.float32(np.arange(11) / 10.0)).all()
-        total_ret += rew.double()
-    assert (np_(tr)[sample] == o_tr).all()
-    st = b.get_state()
+            lid = ob[:, :5 * C].reshape(n, C, 5)
+            assert (lid[:, :, 1:].sum(-1) == 1.0).all(), t
+            assert np.isin(lid[:, :, 0], dist).all(), t
+            assert np.isin(ob[:, 5 * C:5 * C + 2], posv).all(), t
+            assert np.isin(ob[:, 5 * C + 2:], visv).all(), t
+    st = b.get_state(parts=("scalars",))
     s = np_(st["scalars"])
     assert (s[sample] == ov.b.scal).all()
-    # every env truncated exactly once at step 1000 (random policy never finishes)
-    assert (s[:, 7] == 2).all() and (s[:, 2] == 100).all()
+    # a random policy never finishes a map: every episode ends at the truncation
+    assert (s[:, O.S_EPISODE] == 1 + (start + steps) // 1000).all()
+    assert (s[:, O.S_STEP] == (start + steps) % 1000).all()
     b.close()
 
 
