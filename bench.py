@@ -26,6 +26,7 @@ steady state of a long training run); that result is the line's "desync" object.
 import argparse
 import hashlib
 import json
+import math
 import os
 import socket
 import subprocess
@@ -70,6 +71,8 @@ def parse():
                         "fresh episodes, desync as the secondary 'desync' object)")
     p.add_argument("--desync-steps", type=int, default=20000,
                    help="steps of the secondary desynchronized window (0: skip it)")
+    p.add_argument("--prefetch-every", type=int, default=None,
+                   help="steps between prefetched-reset launches (pe_config.prefetch_every; default: the library's)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--selftest", action="store_true",
@@ -270,7 +273,7 @@ def main():
     # rank r owns global env ids [r*n, (r+1)*n) (env_id_offset), no data-path collective
     shard = ShardedPlantOS(n, seed=args.seed, batch_factory=lambda n_, **kw: PlantOSBatch(
         n_, grid_size=G, num_plants=plants, num_obstacles=obstacles, lidar_range=R, lidar_channels=C,
-        device=device, **kw))
+        device=device, prefetch_every=args.prefetch_every, **kw))
     b = shard.batch
     if args.desync:
         desynchronize(torch, b, args.seed)
@@ -294,6 +297,9 @@ def main():
     # graph mode: one graph = `chunk` consecutive pe_step launches; step k of a replay
     # reads action row k % T (plain mode: step t reads row t % T).  K = reps * chunk + rest.
     chunk = min(args.graph, K) if (args.graph > 1 and not gather) else 0
+    pf = b.prefetch_every
+    if chunk > 1 and pf > 0 and chunk % pf:  # every replay must hold the same share of prefetch launches
+        chunk = min(chunk * pf // math.gcd(chunk, pf), max(K, pf))
     graph = None
     if chunk > 1:
         graph = torch.cuda.CUDAGraph()

@@ -237,6 +237,7 @@ int pe_mcts_search(pe_mcts* m, const uint8_t* mask, int32_t* actions, int32_t* r
 int32_t pe_num_envs(const pe_handle* h);
 int32_t pe_kernel_variant(const pe_handle* h);  /* 0 generic, >0 specialized geometry */
 const char* pe_kernel_name(const pe_handle* h);
+int32_t pe_prefetch_every(const pe_handle* h);  /* steps between prefetch launches, 0 = off */
 uint64_t pe_state_bytes(const pe_handle* h);
 
 const char* pe_last_error(void);

@@ -45,7 +45,9 @@ __device__ unsigned long long g_coop_t[8];
 
 constexpr int kCoopWPR = 4;     // row words per lane: G + 2R <= 128
 constexpr int kCoopMaxDone = 8;  // done envs per block up to which the cooperative path is taken
-constexpr int kPrefetchEvery = 64;  // steps between prefetch launches (queue mode)
+constexpr int kPrefetchEvery = 256;  // steps between prefetch launches (queue mode): desynchronized
+                                     // 20x20 step 12.41 / 12.22 / 12.13 / 12.11 us at 64 / 128 / 256 / 512
+                                     // (profiles/r2b_ab_prefetch.jsonl)
 
 // The cooperative path covers the original map generator with one grid row per
 // lane; everything else takes the lane-per-env path.
@@ -516,19 +518,39 @@ __device__ inline Scal coop_gen_map(const Geo& g, const Rules& rl, const Tables*
 }
 
 // _get_info (plantos_env.py:317-336) of env e's current state by one wave
-// (write_info's columns); s: the env's scalars (uniform); wfix: see write_info.
-__device__ inline void coop_write_info(const State& st, const Geo& g, int64_t e, const Scal& s, int32_t* o, int lane,
-                                       int wfix = 0) {
+// (write_info's columns), in two halves so that a caller can issue the row loads
+// before other memory work and wait for them later: coop_info_rows loads lane r's
+// grid row r (sc1 load (L2): the row may hold a word another lane of this wave just
+// stored), coop_info_store reduces and writes the row.  s: the env's scalars
+// (uniform); wfix: see write_info.
+template <int MAXW>
+__device__ __forceinline__ Row4<MAXW> coop_info_rows(const State& st, const Geo& g, int64_t e, int lane) {
+  Row4<MAXW> r{0ull, 0ull, 0ull, 0ull};
+  if (lane < g.G) {
+#pragma unroll
+    for (int w = 0; w < MAXW; ++w)
+      if (MAXW == 1 || w < g.WPR)
+        r.set(w, __hip_atomic_load(st.grid + e * g.gstride + (int64_t)lane * g.WPR + w, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT));
+  }
+  return r;
+}
+
+template <int MAXW>
+__device__ inline void coop_info_store(const State& st, const Geo& g, const Row4<MAXW>& rows, const Scal& s, int32_t* o,
+                                       int lane, int wfix = 0, const Tables* tab = nullptr) {
+  const Tables* T = tab ? tab : st.tab;  // the caller's LDS copy, if it has one
   int th = 0, hy = 0;
-  if (lane < g.G)
-    for (int w = 0; w < g.WPR; ++w) {
-      // sc1 load (L2): the row may hold a word another lane of this wave just stored
-      const uint64_t v = __hip_atomic_load(st.grid + e * g.gstride + (int64_t)lane * g.WPR + w, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t lo = v & kEven64, hi = (v >> 1) & kEven64, real = st.tab->grid_real[w];
-      th += __popcll(lo & hi & real);   // sum(plants.values())     :318
-      hy += __popcll(~lo & hi & real);  // len(plants) - thirsty    :319
-    }
+  if (lane < g.G) {
+#pragma unroll
+    for (int w = 0; w < MAXW; ++w)
+      if (MAXW == 1 || w < g.WPR) {
+        const uint64_t v = rows.get(w);
+        const uint64_t lo = v & kEven64, hi = (v >> 1) & kEven64, real = T->grid_real[w];
+        th += __popcll(lo & hi & real);   // sum(plants.values())     :318
+        hy += __popcll(~lo & hi & real);  // len(plants) - thirsty    :319
+      }
+  }
   th = wave_sum(th) - wfix;
   hy = wave_sum(hy) + wfix;
   int v = 0;
@@ -547,6 +569,12 @@ __device__ inline void coop_write_info(const State& st, const Geo& g, int64_t e,
     default: break;
   }
   if (lane < PE_NINFO) o[lane] = v;
+}
+
+template <int MAXW>
+__device__ inline void coop_write_info(const State& st, const Geo& g, int64_t e, const Scal& s, int32_t* o, int lane,
+                                       int wfix = 0, const Tables* tab = nullptr) {
+  coop_info_store<MAXW>(st, g, coop_info_rows<MAXW>(st, g, e, lane), s, o, lane, wfix, tab);
 }
 
 // Prefetched resets: the map of an env's NEXT reset depends only on (seed, env,
@@ -617,7 +645,8 @@ __device__ __forceinline__ bool coop_take_prefetched(const Prefetch& pf, const G
 // keep: CurriculumWrapper keeps the previous visit counts.
 template <int MAXW>
 __device__ inline Scal coop_apply_reset(const State& st, const Geo& g, int64_t e, Scal s, bool keep,
-                                        const Row4<MAXW>& rw, int lane) {
+                                        const Row4<MAXW>& rw, int lane,
+                                        const Tables* tab = nullptr) {
   if ((s.flags & F_NOROOM) && lane == 0) atomicOr(st.err_bits, F_NOROOM);
   if (lane < g.G) {
     uint64_t* gb = st.grid + e * g.gstride + (int64_t)lane * g.WPR;
@@ -631,7 +660,7 @@ __device__ inline Scal coop_apply_reset(const State& st, const Geo& g, int64_t e
       const int bit = 4 * (s.y + 2);
       const bool rover = lane == s.x && !(s.flags & F_NOROOM);
       for (int w = 0; w < g.NW; ++w) {
-        uint32_t v = st.tab->vis_pad[w];
+        uint32_t v = (tab ? tab : st.tab)->vis_pad[w];
         if (rover && w == (bit >> 5)) v = (v & ~(0xFu << (bit & 31))) | (1u << (bit & 31));
         vb[w] = v;
       }
@@ -649,9 +678,10 @@ __device__ inline Scal coop_apply_reset(const State& st, const Geo& g, int64_t e
 // coop_apply_reset.
 template <int MAXW>
 __device__ inline Scal coop_reset_env(const State& st, const Geo& g, const Rules& rl, int64_t e, uint32_t episode,
-                                      bool keep, Row4<MAXW>& rw, int lane, uint64_t* scr) {
-  const Scal s = coop_gen_map<MAXW>(g, rl, st.tab, rw, rl.env_off + (uint32_t)e, episode, lane, scr);
-  return coop_apply_reset<MAXW>(st, g, e, s, keep, rw, lane);
+                                      bool keep, Row4<MAXW>& rw, int lane, uint64_t* scr,
+                                      const Tables* tab = nullptr) {
+  const Scal s = coop_gen_map<MAXW>(g, rl, tab ? tab : st.tab, rw, rl.env_off + (uint32_t)e, episode, lane, scr);
+  return coop_apply_reset<MAXW>(st, g, e, s, keep, rw, lane, tab);
 }
 
 // build_obs_fresh by one wave from the rows in the lanes' registers: lane i

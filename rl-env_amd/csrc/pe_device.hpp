@@ -98,7 +98,9 @@ struct Prefetch {
   uint4* scal;      // [N] packed scalars the reset produces (before coop_apply_reset)
   uint64_t* grid;   // [N][gstride] grid rows of the new map
   float* obs;       // [N][D] fresh observation of the new episode
-  uint32_t* queue;  // [N] envs that consumed their record (the next batch to generate)
+  uint8_t* flag;    // [N] 1: the env consumed its record (a plain byte store by the step
+                    // kernel -- no returning atomic on its critical path)
+  uint32_t* queue;  // [N] flagged envs, compacted by pe_pf_compact_kernel (the next batch to generate)
   uint32_t* qn;     // [0] queued count, [1] ticket of the generating launch
 };
 

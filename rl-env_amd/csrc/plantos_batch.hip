@@ -197,12 +197,15 @@ __device__ __forceinline__ void load_tables(float* smem, const Tables* tab) {
   for (int k = threadIdx.x; k < kTabFloats; k += blockDim.x) smem[k] = src[k];
 }
 
-// Only the tables the step's hot path reads: dist[0..R], pos[0..G), vis[0..16).
+// The tables the step reads: dist[0..R], pos[0..G), vis[0..16) (hot path) and the
+// pad masks (floats 344.., reset paths: read from LDS there, never from global
+// memory under the obs stores' traffic).
 __device__ __forceinline__ void load_tables_hot(float* smem, const Tables* tab, int G, int R) {
   const float* src = reinterpret_cast<const float*>(tab);
-  const int n = (R + 1) + G + 16;
+  const int n = (R + 1) + G + 16 + (kTabFloats - 344);
   for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    const int f = k <= R ? k : (k < R + 1 + G ? 72 + (k - R - 1) : 328 + (k - R - 1 - G));
+    const int f = k <= R ? k : (k < R + 1 + G ? 72 + (k - R - 1) : (k < R + 1 + G + 16 ? 328 + (k - R - 1 - G)
+                                                                                      : 344 + (k - R - 1 - G - 16)));
     smem[f] = src[f];
   }
 }
@@ -513,7 +516,20 @@ __device__ uint64_t g_stamps[16384 * 8];
 #endif
 #ifdef PE_STAMPS
 #define PE_STAMP(k) PE_STAMP_RAW(k)
+// done-path stamps of the wave running a block's auto-reset (per block)
+__device__ uint64_t g_dstamps[16384 * 8];
+#define PE_DSTAMP(k)                                                                        \
+  do {                                                                                      \
+    uint64_t _t;                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");        \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 16384) g_dstamps[blockIdx.x * 8 + (k)] = _t; \
+  } while (0)
 #else
+#define PE_DSTAMP(k) \
+  do {               \
+  } while (0)
 #define PE_STAMP(k) \
   do {              \
   } while (0)
@@ -573,6 +589,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
     // One done env (the usual case with desynchronized episodes): the commit wave,
     // which holds its scalars, resets it alone -- no staging, one barrier.
     if (wv == CW) {
+      PE_DSTAMP(0);
       const uint64_t dmw = reinterpret_cast<const uint64_t*>(smem)[35];
       const int l = __ffsll((unsigned long long)dmw) - 1;
       const int64_t el = e0 + l;
@@ -580,11 +597,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
       PfLoad<MAXW, KD> pl;
       if (a.pf.scal) coop_load_prefetched<MAXW, KD>(a.pf, g, el, pl, lane);  // in flight from here on
       bool keep = false;
-      if (done) {
-        if (a.ep_ret_out) a.ep_ret_out[e] = ret;
-        if (a.ep_len_out) a.ep_len_out[e] = s.step;
-        if (st.cur) keep = curriculum_on_reset(st.cur, e, rl);  // A2C_training.py:56-95
-      }
+      if (done && st.cur) keep = curriculum_on_reset(st.cur, e, rl);  // A2C_training.py:56-95
       const bool kp = __builtin_amdgcn_readlane((int)keep, l) != 0;
       const int wf = __builtin_amdgcn_readlane((int)wfix, l);
       const Scal sv = unpack(make_uint4((uint32_t)__builtin_amdgcn_readlane((int)sp.x, l),
@@ -598,7 +611,9 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
       // with the curriculum the commit stored this env's rows: they must land before
       // the info reads them and the reset rewrites them
       if (st.cur) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (a.tinfo) coop_write_info(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, wf);
+      PE_DSTAMP(1);
+      if (a.tinfo) coop_write_info<MAXW>(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, wf);
+      PE_DSTAMP(2);
       Row4<MAXW> rw;
       Scal ns;
       asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
@@ -609,15 +624,15 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane, scr);
         coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
       }
-      if (a.pf.scal && lane == 0) {  // its next map goes into the next generating batch
-        const uint32_t q = atomicAdd(a.pf.qn, 1u);
-        if (q < (uint32_t)a.n) a.pf.queue[q] = (uint32_t)el;
-      }
+      PE_DSTAMP(3);
+      if (a.pf.scal && lane == 0) a.pf.flag[el] = 1;  // its next map goes into the next generating batch
+      PE_DSTAMP(4);
       if (done) {  // lane l: program order after its commit stores
         s = ns;
         st.ep_ret[e] = 0.0;
         st.scal[e] = pack(s);
       }
+      PE_DSTAMP(5);
     }
     __syncthreads();  // the fresh obs row is in the tile
     __builtin_amdgcn_s_waitcnt(0x0F70);  // see the end of the path below
@@ -634,13 +649,10 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
     // its own lane, in program order.
     uint32_t* stage = reinterpret_cast<uint32_t*>(lrow);  // [64][5]: packed scalars, keep
     uint64_t* dmask = reinterpret_cast<uint64_t*>(stage + 5 * kQuadEnvs);
-    uint32_t* qbase = reinterpret_cast<uint32_t*>(dmask + 1);  // first prefetch-queue slot of the block
     const int NWv = blockDim.x >> 6;
     if (wv == CW) {
       bool keep = false;
       if (done) {
-        if (a.ep_ret_out) a.ep_ret_out[e] = ret;
-        if (a.ep_len_out) a.ep_len_out[e] = s.step;
         if (st.cur) keep = curriculum_on_reset(st.cur, e, rl);  // A2C_training.py:56-95
         stage[5 * lane] = sp.x;
         stage[5 * lane + 1] = sp.y;
@@ -649,12 +661,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         stage[5 * lane + 4] = (uint32_t)keep | ((uint32_t)wfix << 1);
       }
       const uint64_t dm = __ballot(done);
-      if (lane == 0) {
-        *dmask = dm;
-        // one queue reservation per block (a whole batch resetting at once would
-        // otherwise serialize 65536 atomics on one word)
-        if (a.pf.scal) *qbase = atomicAdd(a.pf.qn, (uint32_t)__popcll(dm));
-      }
+      if (lane == 0) *dmask = dm;
       // with the curriculum, the commit's grid / visit stores of a done env
       // (watering, the carried visit) must land before other waves read its rows
       // (terminal info) and write new ones; otherwise it made none (see the commit)
@@ -685,7 +692,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         // the prefetched record's loads go out first, the terminal info's after them
         PfLoad<MAXW, KD> pl;
         if (a.pf.scal) coop_load_prefetched<MAXW, KD>(a.pf, g, el, pl, lane);
-        if (a.tinfo) coop_write_info(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, kw >> 1);
+        if (a.tinfo) coop_write_info<MAXW>(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, kw >> 1);
         Row4<MAXW> rw;
         Scal ns;
         asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
@@ -696,10 +703,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
           ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane, scr);
           coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
         }
-        if (a.pf.scal && lane == 0) {  // its next map goes into the next generating batch
-          const uint32_t q = *qbase + (uint32_t)k;
-          if (q < (uint32_t)a.n) a.pf.queue[q] = (uint32_t)el;
-        }
+        if (a.pf.scal && lane == 0) a.pf.flag[el] = 1;  // its next map goes into the next generating batch
         const uint4 np = pack(ns);
         if (lane == 0) {
           stage[5 * l] = np.x;
@@ -745,8 +749,6 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
       float* t = a.tobs + e * g.D;
       for (int k = 0; k < g.D; ++k) t[k] = row[k];
     }
-    if (a.ep_ret_out) a.ep_ret_out[e] = ret;
-    if (a.ep_len_out) a.ep_len_out[e] = s.step;
     PE_RSTAMP(1);
     if (a.tinfo) write_info(a.st, a.g, ltab, e, s, a.tinfo + e * PE_NINFO, wfix);
     PE_RSTAMP(2);
@@ -782,10 +784,12 @@ __device__ __forceinline__ void quad_done_obs(const void* ka, int tile_off, int 
 }
 
 template <int C, int R, bool ONEWORD, int NW>
-__global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : (ONEWORD ? 1 : 4)) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs; multi-word NW=4: <= 128 VGPRs (4 workgroups per CU: G=25 13.1 -> 10.5 us)
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs; NW=4: <= 128 VGPRs (4 workgroups per CU: G=25 13.1 -> 10.5 us; 1-word C16: 122 -> 104 VGPRs)
   constexpr int NR = 2 * R + 3, NV = 7, EPB = kQuadEnvs, CW = NW - 1;  // CW: commit wave
+
   static_assert(C % NW == 0, "rays must split evenly over the waves");
   static_assert(ONEWORD || R <= 14, "funnel-shifted window row must hold 2R+5 cells");
+  static_assert(ONEWORD || R >= 2, "the watered cell's byte must lie in the window row");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* tdist = smem;
   float* tpos = smem + 72;
@@ -814,18 +818,17 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : (ONEWORD ? 1 : 4)) void pe_s
   const int le = threadIdx.x / LT, sub = threadIdx.x % LT;
   const int64_t el = e0 + le;
   const bool llive = el < a.n;
-  uint4 sw = make_uint4(0u, 0u, 0u, 0u), lw = make_uint4(0u, 0u, 0u, 0u);
-  int64_t action = 0;
-  double ret = 0.0;
-  if (live) {
-    sw = st.scal[e];
-    action = a.act_bytes == 8 ? reinterpret_cast<const int64_t*>(a.actions)[e]
-                              : (int64_t)reinterpret_cast<const int32_t*>(a.actions)[e];
-    if (wv == CW) ret = st.ep_ret[e];
-  }
-  double cthr = 0.0;
-  if (st.cur && live && wv == CW) cthr = st.cur[e].thr;  // CurriculumWrapper threshold
-  if (llive) lw = st.scal[el];
+  // Every round-1 load unconditional (indices clamped into the batch; the values of
+  // lanes past its end are never used): a load inside a branch whose value merges
+  // after it is waited for right there -- the 4-byte action load used to be, before
+  // the loader scalars were even issued, i.e. two memory round trips instead of one.
+  const int64_t ec = live ? e : (int64_t)a.n - 1, elc = llive ? el : (int64_t)a.n - 1;
+  const uint4 sw = st.scal[ec];
+  const int ash = a.act_bytes == 8 ? 1 : 0;  // 8-byte actions: two words, low first
+  const int32_t* ap = reinterpret_cast<const int32_t*>(a.actions);
+  const int32_t alo = ap[ec << ash], ahi = ap[(ec << ash) + ash];
+  double ret = st.ep_ret[wv == CW ? ec : 0];  // (the commit wave's; the others read one shared word)
+  const uint4 lw = st.scal[elc];
   if constexpr ((kAblate & 64) != 0) {  // diagnostic only: whole-block streaming probe
     const uint4* gsrc = reinterpret_cast<const uint4*>(st.grid + e0 * g.gstride);
     const uint4* vsrc = reinterpret_cast<const uint4*>(st.vis + e0 * g.vstride);
@@ -842,6 +845,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : (ONEWORD ? 1 : 4)) void pe_s
   if ((int)(s.x + lw.x) == -12345) g_stamps[0] = 1;  // consume round 1 before the stamp
 #endif
   PE_STAMP(1);
+  const int64_t action = ash ? (int64_t)(((uint64_t)(uint32_t)ahi << 32) | (uint32_t)alo) : (int64_t)alo;
   bool mv = false, water = false, bad = false;
   int dxm = 0, dym = 0;
   if (action < 4) {                                              // plantos_env.py:166
@@ -863,11 +867,9 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : (ONEWORD ? 1 : 4)) void pe_s
   const int ybv = s.y > 0 ? s.y - 1 : 0;
   const uint64_t* gb = st.grid + e * g.gstride;
   const int cell_o = s.x * g.G + s.y, cell_n = nx * g.G + nyc;
-  const int pbw = (4 * (nyc + 2)) >> 5;  // word of the target's visit nibble
 
   // ---- round 2: window rows of env le -> LDS [row][env] (loader role)
-  uint32_t vraw = 0u, eo = 0u, en = 0u;
-  uint64_t craw = 0ull;
+  uint32_t eo = 0u, en = 0u;
   if (llive && !(kAblate & 4)) {
     const int lx = (int)(lw.x & 0xFF), ly = (int)((lw.x >> 8) & 0xFF);
     const uint64_t* lgb = st.grid + el * g.gstride;
@@ -981,15 +983,16 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : (ONEWORD ? 1 : 4)) void pe_s
       }
     }
   }
-  if (live && wv == CW) {  // what the state commit needs (lane = env)
-    if (inb) {
-      vraw = st.vis[e * g.vstride + (int64_t)nx * g.NW + pbw];
-      if (s.flags & F_EXPL_BITMAP) {
-        eo = st.expl[e * g.estride + (cell_o >> 5)];
-        en = st.expl[e * g.estride + (cell_n >> 5)];
-      }
+  // what the state commit needs beyond the window rows (lane = env): only in the
+  // curriculum / injected-state modes (the visit and grid words it rewrites are
+  // rebuilt from the window rows, see the commit)
+  double cthr = 0.0;
+  if (live && wv == CW) {
+    if (st.cur) cthr = st.cur[e].thr;  // CurriculumWrapper threshold
+    if (inb && (s.flags & F_EXPL_BITMAP)) {
+      eo = st.expl[e * g.estride + (cell_o >> 5)];
+      en = st.expl[e * g.estride + (cell_n >> 5)];
     }
-    if (!ONEWORD && water) craw = gb[(int64_t)s.x * g.WPR + ((2 * (s.y + R)) >> 6)];
   }
 #ifdef PE_STAMPS
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -1095,8 +1098,13 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : (ONEWORD ? 1 : 4)) void pe_s
       wfix = watered && done && a.autoreset && !st.cur;
       if (!(done && a.autoreset && !st.cur)) {
         if (ok) {
-          const int pb = (4 * (ny + 2)) & 31;
-          st_wt(st.vis + e * g.vstride + (int64_t)nx * g.NW + pbw, (vraw & ~(0xFu << pb)) | (nib << pb));
+          // the byte holding the target's visit nibble (padded column p), rebuilt from
+          // the window of row nx in LDS (padded nibbles ybv..ybv+7 hold both of its
+          // nibbles): one byte store, no read of the word from memory
+          const int p = ny + 2, b = p >> 1;
+          const uint32_t wnew = (lvis[(3 + dxm) * EPB + lane] & ~(0xFu << (4 * (p - ybv)))) | (nib << (4 * (p - ybv)));
+          st_wt(reinterpret_cast<uint8_t*>(st.vis + e * g.vstride + (int64_t)nx * g.NW) + b,
+                (uint8_t)(wnew >> (4 * (2 * b - ybv))));
           visit_bump_exact(st, g, e, cell_n, n);
           if (s.flags & F_EXPL_BITMAP) {
             uint32_t* ep_o = st.expl + e * g.estride + (cell_o >> 5);
@@ -1110,7 +1118,12 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : (ONEWORD ? 1 : 4)) void pe_s
           if constexpr (ONEWORD) {
             st_wt(const_cast<uint64_t*>(gb) + ox, (uint64_t)(lrow[(R + 1) * EPB + lane] & ~(1ull << bit)));  // code 3 -> 2
           } else {
-            st_wt(const_cast<uint64_t*>(gb) + (int64_t)ox * g.WPR + (bit >> 6), (uint64_t)(craw & ~(1ull << (bit & 63))));
+            // the byte holding the cell's code (padded column c; its 4 cells lie in the
+            // window of row x, padded columns yb..yb+31, for R >= 2)
+            const int c = s.y + R, B = c >> 2;
+            const uint64_t wr = lrow[(R + 1) * EPB + lane] & ~(1ull << (2 * (c - yb)));  // code 3 -> 2
+            st_wt(reinterpret_cast<uint8_t*>(const_cast<uint64_t*>(gb) + (int64_t)ox * g.WPR) + B,
+                  (uint8_t)(wr >> (2 * (4 * B - yb))));
           }
         }
       }
@@ -1118,8 +1131,15 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : (ONEWORD ? 1 : 4)) void pe_s
       st_wt(a.reward + e, (float)rew);
       st_wt(a.term + e, (uint8_t)term);
       st_wt(a.trunc + e, (uint8_t)trunc);
-      st_wt(st.ep_ret + e, ret);
-      st_wt(st.scal + e, pack(s));
+      if (done) {  // Monitor's episode return / length of the ended episode
+        if (a.ep_ret_out) st_wt(a.ep_ret_out + e, ret);
+        if (a.ep_len_out) st_wt(a.ep_len_out + e, (int32_t)s.step);
+      }
+      // an env about to be auto-reset: its reset path stores the new episode's scalars
+      if (!(done && a.autoreset && !st.cur)) {
+        st_wt(st.ep_ret + e, ret);
+        st_wt(st.scal + e, pack(s));
+      }
     }
   }
   PE_STAMP(4);
@@ -1146,12 +1166,12 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : (ONEWORD ? 1 : 4)) void pe_s
   // auto-reset slow path, out of line (its registers stay off the hot path)
   static_assert(2 * C * R <= (NR * 8 + NV * 4) * EPB, "LIDAR offset tables must fit the window region");
   static_assert(5 * 4 * EPB + 8 <= (NR * 8 + NV * 4) * EPB, "reset staging must fit the window region");
+  const int64_t valid = a.n - e0 < EPB ? a.n - e0 : EPB;
   if (__builtin_expect(any_done, 0)) {  // cold: laid out after the hot path
-    const uint4 ns = quad_done_path<NW, ONEWORD, (5 * C + 27 + 63) / 64>(kernargs(), quad_tile_off<R>(), C, R, lane, wv, CW, e0, done,
-                                                 pack(s), ret, ndone, wfix);
+    const uint4 ns = quad_done_path<NW, ONEWORD, (5 * C + 27 + 63) / 64>(kernargs(), quad_tile_off<R>(), C, R, lane, wv,
+                                                                       CW, e0, done, pack(s), ret, ndone, wfix);
     s = unpack(ns);
   }
-  const int64_t valid = a.n - e0 < EPB ? a.n - e0 : EPB;
   // the obs tile goes out through the waves other than the commit wave: its state
   // stores are still in flight (no fence at the barrier above), and the compiler
   // would make every iteration of its store loop wait for them (s_waitcnt vmcnt(0)
@@ -1211,6 +1231,24 @@ __global__ __launch_bounds__(256) void pe_reset_coop_kernel(StepArgs a) {
     if (a.obs) coop_fresh_obs<MAXW>(g, rw, ns, a.obs + e * g.D, tdist, tpos, tvis, a.st.ldx, a.st.ldy, lane);
   } else if (a.obs && lane == 0) {
     build_obs_generic(a, e, s.x, s.y, a.obs + e * g.D, tdist, tpos, tvis, a.st.ldx, a.st.ldy);
+  }
+}
+
+// The envs flagged by step kernels since the last prefetch launch, compacted into
+// pf.queue (one wave per 64 envs, one atomic per wave with a flagged env), flags
+// cleared.  Runs right before the queue-mode prefetch launch, on the same stream.
+__global__ __launch_bounds__(256) void pe_pf_compact_kernel(Prefetch pf, int n) {
+  const int lane = threadIdx.x & 63;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool f = e < n && pf.flag[e] != 0;
+  const uint64_t m = __ballot(f);
+  if (m == 0ull) return;  // wave-uniform
+  uint32_t base = 0u;
+  if (lane == 0) base = atomicAdd(pf.qn, (uint32_t)__popcll(m));
+  base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+  if (f) {
+    pf.queue[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)e;
+    pf.flag[e] = 0;
   }
 }
 
@@ -1625,6 +1663,10 @@ int launch_prefetch(const pe_handle* h, hipStream_t s, int all) {
   StepArgs a = base_args(h);
   const unsigned nb = (unsigned)((h->n + 3) / 4);
   dim3 grid(all ? nb : std::min(nb, (unsigned)h->pf_blocks)), block(256);
+  if (!all) {
+    hipLaunchKernelGGL(pe_pf_compact_kernel, dim3((unsigned)((h->n + 255) / 256)), dim3(256), 0, s, h->pf, h->n);
+    PE_HIP(hipGetLastError());
+  }
   const size_t lds = sizeof(float) * (size_t)kTabFloats + 4 * 8 * (size_t)coop_scratch_words(h->g.G, h->g.WPR);
   if (h->g.WPR == 1)
     hipLaunchKernelGGL(pe_prefetch_kernel<1>, grid, block, lds, s, a, all);
@@ -1902,6 +1944,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
     };
     const size_t p_scal = pcarve(n * sizeof(uint4)), p_grid = pcarve(n * (size_t)g.gstride * 8);
     const size_t p_obs = pcarve(n * (size_t)g.D * 4), p_q = pcarve(n * 4), p_qn = pcarve(2 * 4);
+    const size_t p_flag = pcarve(n);
     if (hipMalloc(&h->pf_mem, po) != hipSuccess || hipMemset(h->pf_mem, 0, po) != hipSuccess) {
       if (h->pf_mem) (void)hipFree(h->pf_mem);
       (void)hipFree(h->mem);
@@ -1916,6 +1959,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
     h->pf.obs = reinterpret_cast<float*>(pb + p_obs);
     h->pf.queue = reinterpret_cast<uint32_t*>(pb + p_q);
     h->pf.qn = reinterpret_cast<uint32_t*>(pb + p_qn);
+    h->pf.flag = reinterpret_cast<uint8_t*>(pb + p_flag);
     const size_t plds = sizeof(float) * (size_t)kTabFloats + 4 * 8 * (size_t)coop_scratch_words(G, g.WPR);
     int per_cu = 0;
     hipError_t oe = g.WPR == 1
@@ -2148,6 +2192,14 @@ int pe_poll_errors(pe_handle* h, int32_t* bits, void* stream) {
   return PE_OK;
 }
 
+#ifdef PE_STAMPS
+int pe_debug_dstamps(uint64_t* host, int64_t count) {
+  if (count > 16384 * 8) count = 16384 * 8;
+  PE_HIP(hipDeviceSynchronize());
+  PE_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dstamps), (size_t)count * 8, 0, hipMemcpyDeviceToHost));
+  return PE_OK;
+}
+#endif
 #if defined(PE_STAMPS) || defined(PE_STAMPS_RESET)
 int pe_debug_stamps(uint64_t* host, int64_t count) {
   if (count > 16384 * 8) count = 16384 * 8;
@@ -2160,6 +2212,7 @@ int pe_debug_stamps(uint64_t* host, int64_t count) {
 int32_t pe_num_envs(const pe_handle* h) { return h ? h->n : 0; }
 int32_t pe_kernel_variant(const pe_handle* h) { return h ? h->variant : -1; }
 const char* pe_kernel_name(const pe_handle* h) { return h ? h->kname : ""; }
+int32_t pe_prefetch_every(const pe_handle* h) { return h ? h->pf_every : 0; }
 uint64_t pe_state_bytes(const pe_handle* h) { return h ? (uint64_t)h->bytes : 0; }
 
 }  // extern "C"

@@ -36,7 +36,7 @@ def map_algo_id(name):
 EXPORTS = [
     "pe_default_config", "pe_obs_dim", "pe_create", "pe_destroy", "pe_seed", "pe_reset", "pe_step",
     "pe_get_info", "pe_get_state", "pe_set_state", "pe_load_maps", "pe_synth_actions", "pe_poll_errors",
-    "pe_num_envs", "pe_kernel_variant", "pe_kernel_name", "pe_state_bytes", "pe_last_error",
+    "pe_num_envs", "pe_kernel_variant", "pe_kernel_name", "pe_prefetch_every", "pe_state_bytes", "pe_last_error",
     "pe_pystream_create", "pe_pystream_next", "pe_pystream_getrandbits32", "pe_pystream_destroy",
     "pe_curriculum_enable", "pe_curriculum_disable", "pe_curriculum_get",
     "pe_mcts_create", "pe_mcts_destroy", "pe_mcts_seed", "pe_mcts_set_rng", "pe_mcts_get_rng", "pe_mcts_search",
@@ -96,6 +96,8 @@ def lib():
     L.pe_kernel_variant.argtypes = [P]
     L.pe_kernel_variant.restype = I32
     L.pe_kernel_name.argtypes = [P]
+    L.pe_prefetch_every.argtypes = [P]
+    L.pe_prefetch_every.restype = I32
     L.pe_kernel_name.restype = ctypes.c_char_p
     L.pe_state_bytes.argtypes = [P]
     L.pe_state_bytes.restype = U64

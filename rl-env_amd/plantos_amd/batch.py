@@ -127,6 +127,12 @@ class PlantOSBatch:
         return C.lib().pe_kernel_name(self.handle).decode()
 
     @property
+    def prefetch_every(self):
+        """Steps between the launches that generate next-episode maps ahead of time
+        (0: no prefetched resets for this geometry / configuration)."""
+        return int(C.lib().pe_prefetch_every(self.handle))
+
+    @property
     def kernel_variant(self):
         return int(C.lib().pe_kernel_variant(self.handle))
 

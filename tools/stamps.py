@@ -23,10 +23,10 @@ NAMES = ["entry", "round1", "round2+lds", "barrier", "compute", "barrier_or", "s
 
 def build(ablate=0):
     so = SO if not ablate else SO.replace(".so", f"_abl{ablate}.so")
-    os.makedirs(os.path.dirname(so), exist_ok=True)
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                    "-DPE_STAMPS", "-DPE_DEBUG_KNOBS", f"-DPE_ABLATE={ablate}", "-o", so,
-                    os.path.join(REPO, "rl-env_amd", "csrc", "plantos_batch.hip")], check=True)
+    sys.path.insert(0, os.path.join(REPO, "rl-env_amd"))
+    import build as B
+    B.build(force=True, out=so, extra_flags=["-DPE_STAMPS", "-DPE_DEBUG_KNOBS", f"-DPE_ABLATE={ablate}"],
+            obj_dir=os.path.join(os.path.dirname(so), f"obj{ablate}"))
     print(so)
 
 
@@ -51,17 +51,26 @@ def run(argv):
     P, O = (10, 12) if G <= 32 else (100, 120)
     b = PlantOSBatch(n, grid_size=G, num_plants=P, num_obstacles=O, lidar_range=6, lidar_channels=C,
                      device="cuda:0")
+    desync = "--desync" in argv
+    if desync:  # every env at its own step count (bench.py --desync)
+        st = b.get_state()
+        sc = st["scalars"]
+        g = torch.Generator(device="cpu").manual_seed(1)
+        sc[:, _capi.PE_S_STEP] = torch.randint(0, 1000, (n,), generator=g, dtype=torch.int32).to(sc.device)
+        b.set_state(scalars=sc)
     acts = torch.empty((64, n), dtype=torch.int32, device="cuda:0")
     for t in range(64):
         b.synth_actions(0, t, out=acts[t])
     for t in range(300):
         b.step(acts[t % 64])
     torch.cuda.synchronize()
-    b.step(acts[7])
+    _, _, te, tr = b.step(acts[7])
     torch.cuda.synchronize()
+    done = (te.bool() | tr.bool()).cpu().numpy()
     L = _capi.lib()
     L.pe_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
-    nw = (n + 63) // 64 * (int(os.environ.get("PE_QUAD_WAVES", "8")))
+    NWQ = int(os.environ.get("PE_QUAD_WAVES", "4"))
+    nw = (n + 63) // 64 * NWQ
     buf = np.zeros(nw * 8, np.uint64)
     _capi.check(L.pe_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.size), "stamps")
     st = buf.reshape(nw, 8).astype(np.int64)
@@ -74,6 +83,27 @@ def run(argv):
            "phase_ns": {f"{NAMES[k - 1]}->{NAMES[k]}": {"p50": int(np.median(rel[:, k] - rel[:, k - 1])),
                                                          "p90": int(np.percentile(rel[:, k] - rel[:, k - 1], 90))}
                         for k in range(1, 8)}}
+    if desync:
+        nb = (n + 63) // 64
+        dpb = np.add.reduceat(done.astype(np.int64), np.arange(0, n, 64))
+        L.pe_debug_dstamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+        dbuf = np.zeros(nb * 8, np.uint64)
+        _capi.check(L.pe_debug_dstamps(dbuf.ctypes.data_as(ctypes.c_void_p), dbuf.size), "dstamps")
+        ds = (dbuf.reshape(nb, 8).astype(np.int64) - t0) * 10
+        cw = rel.reshape(nb, NWQ, 8)[:, NWQ - 1, :]  # the commit wave of every block
+        one = np.where(dpb == 1)[0]
+        none = np.where(dpb == 0)[0]
+        out["desync"] = {
+            "blocks_done": {int(k): int((dpb == k).sum()) for k in np.unique(dpb)},
+            "commit_wave_no_done_p50": {NAMES[k]: int(np.median(cw[none, k])) for k in range(8)},
+            "commit_wave_one_done_p50": {NAMES[k]: int(np.median(cw[one, k])) for k in range(8)},
+            "done_path_p50": {f"d{k}": int(np.median(ds[one, k])) for k in range(6)},
+            "done_path_p90": {f"d{k}": int(np.percentile(ds[one, k], 90)) for k in range(6)},
+            "block_end_no_done_p50": int(np.median(rel.reshape(nb, NWQ, 8)[none, :, 7].max(1))),
+            "block_end_one_done_p50": int(np.median(rel.reshape(nb, NWQ, 8)[one, :, 7].max(1))),
+            "block_end_one_done_p90": int(np.percentile(rel.reshape(nb, NWQ, 8)[one, :, 7].max(1), 90)),
+            "done_points": "single-done path (commit wave): d0 entry, d1 tobs copied, d2 info written, "
+                           "d3 reset taken+applied, d4 queue flag, d5 scalars stored"}
     print(json.dumps(out))
 
 
