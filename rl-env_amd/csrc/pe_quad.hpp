@@ -22,6 +22,8 @@
 //   barrier (+ auto-reset slow path in the commit wave if any env is done)
 //   the 64*NW threads stream the [64 x D] obs tile to HBM with 16-B stores.
 #pragma once
+#include <type_traits>
+
 #include "pe_device.hpp"
 
 namespace pe {
@@ -59,51 +61,65 @@ __device__ __forceinline__ uint64_t quad_row(const uint64_t* gb, const Geo& g, i
   }
 }
 
+// LDS table words the sector rays read (in the tables' dist[] region, which holds
+// dist[0..R]): dist[R+1] = 1.0 (nothing hit), and at kOneHotF the one-hot rows of
+// the 4 entity codes as float4 (16-B aligned).
+constexpr int kOneHotF = 48;
+
 // Rays [W*C/NW, (W+1)*C/NW) of one env (the sector of wave W): first hit over the
 // post-move window rows read from LDS (row k of the [row][env] block = grid row
-// x-R-1+k), written as obs[5i .. 5i+4] (plantos_env.py:260-292).
+// x-R-1+k), written as obs[5i .. 5i+4] (plantos_env.py:260-292).  Per ray the R
+// probe codes are packed 2 bits each (probe r at bits 2(r-1)), so the first hit is
+// one find-first-set over their nonzero bits (a sentinel at bit 2R: nothing hit,
+// range R, entity EMPTY), and its distance and one-hot come from LDS tables:
+// ~3 VALU per probe instead of a compare-and-select chain per probe and per float.
 template <int C, int R, int NW, int W>
-__device__ __forceinline__ void quad_rays(const uint64_t* lrow, int lane, int kc, int sh, bool watered, float* row) {
+__device__ __forceinline__ void quad_rays(const uint64_t* lrow, int lane, int kc, int sh, bool watered, float* row,
+                                          const float* tdist) {
   constexpr int I0 = W * C / NW, I1 = (W + 1) * C / NW;
   constexpr int LO = ray_dx_min<C, R>(I0, I1), HI = ray_dx_max<C, R>(I0, I1);
-  uint64_t win[HI - LO + 1];
+  static_assert(2 * R + 1 <= 31, "packed probe codes + sentinel fit 32 bits");
+  // the window cells yp-R .. yp+R of a row: 2(2R+1) bits (32-bit words up to R = 7)
+  using WT = typename std::conditional<(4 * R + 2 <= 32), uint32_t, uint64_t>::type;
+  WT win[HI - LO + 1];
 #pragma unroll
-  for (int j = 0; j <= HI - LO; ++j) win[j] = lrow[(kc + LO + j) * kQuadEnvs + lane] >> sh;
+  for (int j = 0; j <= HI - LO; ++j) win[j] = (WT)(lrow[(kc + LO + j) * kQuadEnvs + lane] >> sh);
   if constexpr (LO <= 0 && HI >= 0) {
     // watering turned the rover's cell thirsty -> hydrated (code 3 -> 2)
-    if (watered) win[-LO] &= ~(1ull << (2 * R));
+    if (watered) win[-LO] &= ~((WT)1 << (2 * R));
   }
+  constexpr uint32_t kNZ = 0x55555555u & ((1u << (2 * R)) - 1u);
+  const float4* tone = reinterpret_cast<const float4*>(tdist + kOneHotF);
   using T = LidarTab<C, R>;
 #pragma unroll
   for (int i = I0; i < I1; ++i) {
-    float dist = 1.0f;  // nothing hit: float(R / R), plantos_env.py:262
-    int ent = EMPTY;
+    uint32_t pk = 0u;
 #pragma unroll
-    for (int r = R; r >= 1; --r) {
+    for (int r = 1; r <= R; ++r) {
       const int dx = T::dx[i][r - 1], dy = T::dy[i][r - 1];
-      const int cd = (int)((win[dx - LO] >> (2 * (dy + R))) & 3u);
-      if (cd != EMPTY) {
-        dist = (float)((double)r / (double)R);  // float(r / R), plantos_env.py:288
-        ent = cd;
-      }
+      pk |= (uint32_t)((win[dx - LO] >> (2 * (dy + R))) & 3u) << (2 * (r - 1));
     }
-    row[5 * i] = dist;
-    row[5 * i + 1] = ent == 0 ? 1.0f : 0.0f;
-    row[5 * i + 2] = ent == 1 ? 1.0f : 0.0f;
-    row[5 * i + 3] = ent == 2 ? 1.0f : 0.0f;
-    row[5 * i + 4] = ent == 3 ? 1.0f : 0.0f;
+    const uint32_t nz = ((pk | (pk >> 1)) & kNZ) | (1u << (2 * R));
+    const int f = __builtin_ctz(nz);         // 2(r-1) of the first hit, 2R if none
+    const int ent = (int)((pk >> f) & 3u);   // its code (EMPTY if none)
+    row[5 * i] = tdist[(f >> 1) + 1];        // float(r / R), plantos_env.py:288 (R/R if none)
+    const float4 oh = tone[ent];
+    row[5 * i + 1] = oh.x;
+    row[5 * i + 2] = oh.y;
+    row[5 * i + 3] = oh.z;
+    row[5 * i + 4] = oh.w;
   }
 }
 
 // Wave-uniform dispatch of the sector code (wv comes from readfirstlane).
 template <int C, int R, int NW, int W = 0>
 __device__ __forceinline__ void sector_rays(int wv, const uint64_t* lrow, int lane, int kc, int sh, bool watered,
-                                            float* row) {
+                                            float* row, const float* tdist) {
   if constexpr (W < NW) {
     if (wv == W)
-      quad_rays<C, R, NW, W>(lrow, lane, kc, sh, watered, row);
+      quad_rays<C, R, NW, W>(lrow, lane, kc, sh, watered, row, tdist);
     else
-      sector_rays<C, R, NW, W + 1>(wv, lrow, lane, kc, sh, watered, row);
+      sector_rays<C, R, NW, W + 1>(wv, lrow, lane, kc, sh, watered, row, tdist);
   }
 }
 

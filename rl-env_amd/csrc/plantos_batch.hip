@@ -839,6 +839,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
     reinterpret_cast<uint32_t*>(smem + quad_tile_off<R>())[threadIdx.x] = acc;
   }
   load_tables_hot(smem, st.tab, a.g.G, R);
+  // the sector rays' tables (pe_quad.hpp quad_rays): dist[R+1] = 1.0, one-hot rows
+  static_assert(R + 2 <= kOneHotF && kOneHotF + 16 <= 70, "ray tables inside dist[], below the done mask");
+  if (threadIdx.x < 16) smem[kOneHotF + threadIdx.x] = (threadIdx.x >> 2) == (threadIdx.x & 3) ? 1.0f : 0.0f;
+  if (threadIdx.x == 16) smem[R + 1] = 1.0f;
   const Tables* ltab = reinterpret_cast<const Tables*>(smem);
   Scal s = unpack(sw);
 #ifdef PE_STAMPS
@@ -1045,7 +1049,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
     const int kc = dxv + R + 1;
     const int sh = 2 * (yp - yb);
     const int vs = 4 * (yp - ybv);
-    if constexpr (!(kAblate & 2)) sector_rays<C, R, NW>(wv, lrow, lane, kc, sh, watered, row);
+    if constexpr (!(kAblate & 2)) sector_rays<C, R, NW>(wv, lrow, lane, kc, sh, watered, row, tdist);
     // slice rows and position go to the non-commit waves (the commit wave is the laggard)
     if (wv != CW)
       for (int lx = wv; lx < 5; lx += NW - 1) quad_slice_row(lvis, lane, lx, dxv, vs, ok, nib, C, row, tvis);
