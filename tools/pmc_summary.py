@@ -56,10 +56,14 @@ def main():
     ap.add_argument("--kernel", default="pe_step")
     ap.add_argument("--stats-dir", default=None)
     ap.add_argument("--bench-json", default=None, help="bench line of the profiled run (config)")
+    ap.add_argument("--fetch-dir", default=None, help="FETCH_SIZE pass dir under gpurun_out (tools/gpu_session.sh: pmcf_TAG)")
+    ap.add_argument("--write-dir", default=None, help="WRITE_SIZE pass dir under gpurun_out (tools/gpu_session.sh: pmcw_TAG)")
     a = ap.parse_args()
     g = os.path.join(REPO, "gpurun_out")
-    fetch, meta = per_kernel(os.path.join(g, f"{a.prefix}_fetch_{a.tag}", "run_counter_collection.csv"), "FETCH_SIZE")
-    write, _ = per_kernel(os.path.join(g, f"{a.prefix}_write_{a.tag}", "run_counter_collection.csv"), "WRITE_SIZE")
+    fd = a.fetch_dir or f"{a.prefix}_fetch_{a.tag}"
+    wd = a.write_dir or f"{a.prefix}_write_{a.tag}"
+    fetch, meta = per_kernel(os.path.join(g, fd, "run_counter_collection.csv"), "FETCH_SIZE")
+    write, _ = per_kernel(os.path.join(g, wd, "run_counter_collection.csv"), "WRITE_SIZE")
     names = [k for k in fetch if a.kernel in k]
     if not names:
         raise SystemExit(f"no kernel matching {a.kernel}")
