@@ -787,7 +787,7 @@ template <int C, int R, bool ONEWORD, int NW>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs; NW=4: <= 128 VGPRs (4 workgroups per CU: G=25 13.1 -> 10.5 us; 1-word C16: 122 -> 104 VGPRs)
   constexpr int NR = 2 * R + 3, NV = 7, EPB = kQuadEnvs, CW = NW - 1;  // CW: commit wave
 
-  static_assert(C % NW == 0, "rays must split evenly over the waves");
+  static_assert(C >= NW, "every wave owns a sector of at least one ray");
   static_assert(ONEWORD || R <= 14, "funnel-shifted window row must hold 2R+5 cells");
   static_assert(ONEWORD || R >= 2, "the watered cell's byte must lie in the window row");
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1614,11 +1614,14 @@ size_t lds_bytes(const Geo& g) {
 }
 
 // Step kernel variants.  The quadrant kernels (4 waves x 64 envs per workgroup)
-// are the default for the specialized geometries; the one-lane-per-env kernels
-// stay selectable (PE_STEP_KERNEL=lane) for A/B measurement.
+// are the default for the specialized geometries (compile-time C, R: the LIDAR
+// offsets of lidar_tables.inc); the one-lane-per-env kernels stay selectable
+// (PE_STEP_KERNEL=lane, debug builds) for A/B measurement at C16R6 / C64R6.
 enum Variant {
   V_GENERIC = 0, V_C16R6_1W = 1, V_C16R6 = 2, V_C64R6 = 3,
-  V_QUAD_C16R6_1W = 4, V_QUAD_C16R6 = 5, V_QUAD_C64R6 = 6
+  V_QUAD_C16R6_1W = 4, V_QUAD_C16R6 = 5, V_QUAD_C64R6 = 6,
+  V_QUAD_C10R2_1W = 7, V_QUAD_C10R2 = 8,  // plantos_env.py:25-26 constructor default (G=21: multi-word)
+  V_QUAD_C16R4_1W = 9, V_QUAD_C16R4 = 10  // test_environment.py:24 (G=15, C=16, R=4)
 };
 
 size_t quad_lds_bytes(const Geo& g) {
@@ -1639,12 +1642,18 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((pe_step_quad<CC, RR, OW, 8>), grid, block, lds, s, a);              \
   else                                                                                      \
     hipLaunchKernelGGL((pe_step_quad<CC, RR, OW, 4>), grid, block, lds, s, a);
+#define PE_QUAD4(CC, RR, OW) hipLaunchKernelGGL((pe_step_quad<CC, RR, OW, 4>), grid, block, lds, s, a);
     switch (h->variant) {
       case V_QUAD_C16R6_1W: PE_QUAD(16, 6, true); break;
       case V_QUAD_C16R6: PE_QUAD(16, 6, false); break;
-      default: PE_QUAD(64, 6, false); break;
+      case V_QUAD_C64R6: PE_QUAD(64, 6, false); break;
+      case V_QUAD_C10R2_1W: PE_QUAD4(10, 2, true); break;
+      case V_QUAD_C10R2: PE_QUAD4(10, 2, false); break;
+      case V_QUAD_C16R4_1W: PE_QUAD4(16, 4, true); break;
+      default: PE_QUAD4(16, 4, false); break;
     }
 #undef PE_QUAD
+#undef PE_QUAD4
   } else {
     dim3 grid((unsigned)((h->n + kBlock - 1) / kBlock)), block(kBlock);
     size_t lds = lds_bytes(h->g);
@@ -1714,6 +1723,10 @@ const char* variant_name(int v) {
     case V_QUAD_C16R6_1W: return "pe_step_quad<C16,R6,1word>";
     case V_QUAD_C16R6: return "pe_step_quad<C16,R6>";
     case V_QUAD_C64R6: return "pe_step_quad<C64,R6>";
+    case V_QUAD_C10R2_1W: return "pe_step_quad<C10,R2,1word>";
+    case V_QUAD_C10R2: return "pe_step_quad<C10,R2>";
+    case V_QUAD_C16R4_1W: return "pe_step_quad<C16,R4,1word>";
+    case V_QUAD_C16R4: return "pe_step_quad<C16,R4>";
     default: return "pe_step_kernel<generic>";
   }
 }
@@ -1887,8 +1900,17 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   if (const char* lf = std::getenv("PE_LDS_FLOOR")) h->lds_floor = std::min<size_t>(std::strtoul(lf, nullptr, 10), 160 * 1024);
 #endif
   if (!lane_kernels && h->variant != V_GENERIC) h->variant += V_QUAD_C16R6_1W - V_C16R6_1W;
-  if (is_quad(h->variant) && quad_lds_bytes(g) > 160 * 1024) h->variant -= V_QUAD_C16R6_1W - V_C16R6_1W;
+  // sector kernels of the other specialized geometries (4 waves; no lane-kernel twin)
+  if (!lane_kernels && C == 10 && R == 2 && table_matches<10, 2>(ldx, ldy)) h->variant = V_QUAD_C10R2_1W;
+  if (!lane_kernels && C == 16 && R == 4 && table_matches<16, 4>(ldx, ldy)) h->variant = V_QUAD_C16R4_1W;
+  if (h->variant >= V_QUAD_C10R2_1W) h->quad_waves = 4;
+  // the one-word form (whole padded row in one u64) needs WPR == 1 and 16-B visit
+  // rows (NW == 4: G <= 20); otherwise the multi-word (funnel-shifted) form
+  const bool oneword = g.WPR == 1 && g.NW == 4;
+  if ((h->variant == V_QUAD_C10R2_1W || h->variant == V_QUAD_C16R4_1W) && !oneword) h->variant += 1;
   if (h->variant == V_QUAD_C16R6_1W && g.NW != 4) h->variant = V_C16R6_1W;  // needs 16-B visit rows
+  if (is_quad(h->variant) && quad_lds_bytes(g) > 160 * 1024)
+    h->variant = h->variant <= V_QUAD_C64R6 ? h->variant - (V_QUAD_C16R6_1W - V_C16R6_1W) : V_GENERIC;
   h->kname = variant_name(h->variant);
   // explicit reset-path tuning (pe_config.coop_max_done; -1: the choice above) --
   // applied before the prefetch decision, which depends on it

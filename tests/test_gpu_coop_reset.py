@@ -22,6 +22,8 @@ CFG = {
     "g32": (32, 20, 30, 9, 24),
     "g21": (21, 8, 50, 2, 10),
     "g25": (25, 10, 12, 6, 16),   # the multi-word C16 sector kernel (train_mcts's grid)
+    "g15": (15, 6, 8, 4, 16),     # one-word C16R4 sector kernel (test_environment.py:24)
+    "g12r2": (12, 4, 6, 2, 10),   # one-word C10R2
 }
 
 
@@ -45,6 +47,9 @@ def info_rows(b, idx):
     ("g32", 300, 60, 50, None, None, None, None, False),
     ("g21", 400, 60, 50, None, None, None, None, False),
     ("g25", 600, 80, 60, None, None, None, None, False),
+    ("g15", 600, 80, 60, None, None, None, None, False),
+    ("g12r2", 600, 80, 60, None, None, None, None, False),
+    ("g21", 256, 12, 1, "0", None, None, None, False),        # the constructor default, dense: lane-per-env path
     ("g20", 256, 12, 1, "64", None, None, None, False),       # every env at once through the cooperative path
     ("g64", 128, 12, 1, "0", None, None, None, False),        # every env at once through the lane-per-env path
     ("g20", 256, 12, 1, "8", "0", None, None, False),         # no prefetch: in-kernel map generation

@@ -21,6 +21,17 @@ CFG = {
     "g64r32": (64, 100, 120, 32, 64),
     "g7": (7, 3, 3, 3, 12),
     "g32": (32, 20, 30, 9, 24),
+    "g15": (15, 6, 8, 4, 16),     # test_environment.py:24's custom env (one-word C16R4 sector kernel)
+    "g25r4": (25, 10, 12, 4, 16),  # multi-word C16R4
+    "g12r2": (12, 4, 6, 2, 10),    # one-word C10R2 (g21 = the constructor default: multi-word C10R2)
+}
+
+# which step kernel each geometry runs (pe_kernel_name): the sector kernel wherever a
+# specialization exists, the table-driven kernel otherwise
+KERNELS = {
+    "g20": "pe_step_quad<C16,R6,1word>", "g25": "pe_step_quad<C16,R6>", "g64": "pe_step_quad<C64,R6>",
+    "g21": "pe_step_quad<C10,R2>", "g12r2": "pe_step_quad<C10,R2,1word>", "g15": "pe_step_quad<C16,R4,1word>",
+    "g25r4": "pe_step_quad<C16,R4>",
 }
 
 
@@ -136,8 +147,16 @@ def test_device_reset_matches_oracle_philox(name):
     b.close()
 
 
-@pytest.mark.parametrize("name,n,steps", [("g20", 4096, 1100), ("g21", 1000, 300), ("g7", 777, 400),
-                                          ("g64", 256, 120), ("g64r32", 96, 60), ("g25", 300, 200)])
+@pytest.mark.parametrize("name", sorted(KERNELS))
+def test_kernel_selection(name):
+    b = make(CFG[name], 64)
+    assert b.kernel_name == KERNELS[name]
+    b.close()
+
+
+@pytest.mark.parametrize("name,n,steps", [("g20", 4096, 1100), ("g21", 1000, 1010), ("g7", 777, 400),
+                                          ("g64", 256, 120), ("g64r32", 96, 60), ("g25", 300, 200),
+                                          ("g15", 1000, 1010), ("g25r4", 300, 200), ("g12r2", 500, 300)])
 def test_rollout_parity_device_rng(name, n, steps):
     """Device-rng episodes with synthetic actions, auto-reset included (g20 crosses
     the 1000-step truncation): every output of every step vs the oracle."""

@@ -4,7 +4,8 @@
 # the CPU (tools/ab_build.sh) and travel with the tree.
 #   usage: bash tools/gpu_session.sh TAG step [step ...]
 #   steps: tests | smoke | bench | benchd | bench64 | stats | statsd | stats64 |
-#          pmcf | pmcw | pmcf64 | pmcw64 | stamps | stampsd | ab:<name>:<rounds>:<lib,lib,...>:<bench args with _ for spaces>
+#          pmcf | pmcw | pmcf64 | pmcw64 | stamps | stampsd | benchx:<name>:<args> | statsx:<name>:<args> |
+#          ab:<name>:<rounds>:<lib,lib,...>:<bench args with _ for spaces>
 set -euo pipefail
 TAG=$1
 shift
@@ -46,6 +47,13 @@ for w in "$@"; do
     stamps|stampsd)
       flag=""; [ $w = stampsd ] && flag="--desync"
       timeout -k 10 180 python tools/stamps.py run $flag > $OUT/${w}_$TAG.json 2> $OUT/${w}_$TAG.err ;;
+    benchx:*)  # benchx:<name>:<bench args with _ for spaces>
+      IFS=: read -r _ name args <<< "$w"
+      timeout -k 10 300 python bench.py ${args//_/ } > $OUT/benchx_${name}_$TAG.json 2> $OUT/benchx_${name}_$TAG.err ;;
+    statsx:*)  # statsx:<name>:<bench args with _ for spaces> under rocprofv3 --kernel-trace --stats
+      IFS=: read -r _ name args <<< "$w"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/statsx_${name}_$TAG -o run -- \
+        python3 bench.py ${args//_/ } > $OUT/statsx_${name}_$TAG.json 2> $OUT/statsx_${name}_$TAG.err ;;
     ab:*)
       IFS=: read -r _ name rounds libs args <<< "$w"
       libs=${libs//,/ }  # lib[+VAR=VAL]: ab_bench.sh's lib,VAR=VAL
