@@ -267,60 +267,8 @@ __device__ __forceinline__ void store_tile(const float* rows, float* dst, int va
 }
 
 // ------------------------------------------------------------------ kernels
-__global__ __launch_bounds__(kBlock) void pe_step_kernel(StepArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* tdist = smem;
-  float* tpos = smem + 72;
-  float* tvis = smem + 328;
-  float* rows = smem + kTabFloats;
-  load_tables(smem, a.st.tab);
-  const Tables* ltab = reinterpret_cast<const Tables*>(smem);
-  __syncthreads();
-  const int64_t e0 = (int64_t)blockIdx.x * kBlock;
-  const int64_t e = e0 + threadIdx.x;
-  float* row = rows + threadIdx.x * a.g.DS;
-  if (e < a.n) {
-    int64_t action = a.act_bytes == 8 ? reinterpret_cast<const int64_t*>(a.actions)[e]
-                                       : (int64_t)reinterpret_cast<const int32_t*>(a.actions)[e];
-    Scal s = unpack(a.st.scal[e]);
-    bool term = false, trunc = false;
-    double rew = transition(a, e, s, action, term, trunc);
-    if (a.st.cur) term = curriculum_hit(a.st.cur, e, a.st.cur[e].thr, s.expl, s.total, a.rl.cur_term) || term;
-    double ret = a.st.ep_ret[e] + rew;
-    a.reward[e] = (float)rew;
-    a.term[e] = term;
-    a.trunc[e] = trunc;
-    if (term || trunc) {
-      // terminal outputs of an ended episode; DummyVecEnv.step_wait then resets
-      // and returns the reset obs (autoreset), else the caller resets (pe_load_maps)
-      if (a.tobs) {
-        build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis, a.st.ldx, a.st.ldy);
-        float* t = a.tobs + e * a.g.D;
-        for (int k = 0; k < a.g.D; ++k) t[k] = row[k];
-      }
-      if (a.ep_ret_out) a.ep_ret_out[e] = ret;
-      if (a.ep_len_out) a.ep_len_out[e] = s.step;
-      if (a.tinfo) write_info(a.st, a.g, ltab, e, s, a.tinfo + e * PE_NINFO);
-      if (a.autoreset) {
-        s = reset_env(a.st, a.g, a.rl, ltab, e, s.episode);
-        ret = 0.0;
-      }
-    }
-    a.st.ep_ret[e] = ret;
-    a.st.scal[e] = pack(s);
-    if ((term || trunc) && a.autoreset)  // the reset() obs (fresh visits even if a curriculum carries them)
-      build_obs_fresh(a, a.st.grid + e * a.g.gstride, s, row, tdist, tpos, tvis, a.st.ldx, a.st.ldy);
-    else
-      build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis, a.st.ldx, a.st.ldy);
-  }
-  __syncthreads();
-  const int64_t valid = a.n - e0 < kBlock ? a.n - e0 : kBlock;
-  store_tile(rows, a.obs + e0 * a.g.D, (int)valid, a.g.D, a.g.DS);
-}
-
-
 // Specialized fused step (compile-time C, R): two load rounds per lane, the rest
-// from registers (pe_fast.hpp).  Same semantics as pe_step_kernel + transition().
+// from registers (pe_fast.hpp).  Same semantics as pe_step_wave.
 template <int C, int R, bool ONEWORD>
 __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -543,7 +491,7 @@ __device__ uint64_t g_dstamps[16384 * 8];
 #endif
 
 // Quadrant-split fused step (pe_quad.hpp): 4 waves x 64 envs per workgroup.
-// Same semantics as pe_step_kernel + transition().
+// Same semantics as pe_step_wave.
 template <int R>
 constexpr int quad_tile_off() {
   return (kTabFloats + (2 * R + 3) * kQuadEnvs * 2 + 7 * kQuadEnvs + 3) & ~3;
@@ -1202,6 +1150,320 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   PE_STAMP(7);
 }
 
+// ---------------------------------------------------------------- pe_step_wave
+// The fused step for every geometry without a compile-time sector kernel (any
+// G <= 128, C <= 256, R <= 64; e.g. SURVEY §8(d)'s 64x64 / 64 rays / R=32 stress
+// variant): ONE WAVE PER ENV.  The rover's window -- grid rows x-R-1 .. x+R+1
+// clipped to the map, one contiguous 16-B-aligned span of the env's block, and
+// visit rows x-3 .. x+3 -- is staged into the wave's LDS region with coalesced
+// loads in one round after the scalars; the transition and commit are wave-uniform
+// (scalar loads of the env's scalars / action / return); lane i marches ray i
+// (i+64, ... for C > 64) over LDS (plantos_env.py:260-292), lanes 0..26 build the
+// position and the 5x5 visit slice, and the obs row goes out through LDS as
+// contiguous stores.  A done env's auto-reset is the wave-cooperative one of the
+// sector kernel (prefetched record or in-place map generation, pe_coop.hpp) where
+// coop_reset_ok; otherwise lane 0 runs the serial reset (reset_env).
+// Per-wave LDS: the window words (max(min(G,2R+3)*WPR + 2, G*WPR) u64: also the
+// cooperative reset's scratch), 7 visit rows of NW u32, the D-float obs row.
+__host__ __device__ constexpr int wave_win_words(int G, int R, int WPR) {
+  return ((((G < 2 * R + 3 ? G : 2 * R + 3) * WPR + 2) > G * WPR ? ((G < 2 * R + 3 ? G : 2 * R + 3) * WPR + 2)
+                                                                  : G * WPR) + 1) & ~1;
+}
+__host__ __device__ constexpr int wave_lds_floats(int G, int R, int WPR, int NW, int D) {
+  return 2 * wave_win_words(G, R, WPR) + ((7 * NW + 3) & ~3) + ((D + 3) & ~3);
+}
+constexpr int kWaveEnvs = 4;  // envs (waves) per workgroup
+
+template <int MAXW>  // the cooperative reset's row words (1 or kCoopWPR)
+__global__ __launch_bounds__(64 * kWaveEnvs) void pe_step_wave(StepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const Geo& g = a.g;
+  const Rules& rl = a.rl;
+  const State& st = a.st;
+  const Tables* tab = st.tab;  // global (L1/L2-resident): 4 envs per workgroup would re-load an LDS copy per 4 envs
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t e = (int64_t)blockIdx.x * kWaveEnvs + wv;
+  if (e >= a.n) return;  // wave-uniform; no workgroup barrier below
+  const int G = g.G, R = g.R, WPR = g.WPR, NW = g.NW, D = g.D;
+  float* base = smem + wv * wave_lds_floats(G, R, WPR, NW, D);
+  uint64_t* win = reinterpret_cast<uint64_t*>(base);
+  uint32_t* lvis = reinterpret_cast<uint32_t*>(base + 2 * wave_win_words(G, R, WPR));
+  float* row = base + 2 * wave_win_words(G, R, WPR) + ((7 * NW + 3) & ~3);
+
+  // ---- round 1 (uniform: scalar loads)
+  Scal s = unpack(st.scal[e]);
+  const int64_t action = a.act_bytes == 8 ? reinterpret_cast<const int64_t*>(a.actions)[e]
+                                          : (int64_t)reinterpret_cast<const int32_t*>(a.actions)[e];
+  double ret = st.ep_ret[e];
+  bool mv = false, water = false, bad = false;
+  int dxm = 0, dym = 0;
+  if (action < 4) {                                        // plantos_env.py:166
+    const int64_t ai = action < 0 ? action + 4 : action;   // Python negative index
+    if (ai < 0) {
+      bad = true;                                          // reference IndexError
+    } else {
+      mv = true;                                           // :186 N,E,S,W
+      dxm = ai == 0 ? -1 : (ai == 2 ? 1 : 0);
+      dym = ai == 1 ? 1 : (ai == 3 ? -1 : 0);
+    }
+  } else {
+    water = true;
+  }
+  const int nx = s.x + dxm, ny = s.y + dym;
+  const bool inb = mv && nx >= 0 && nx < G && ny >= 0 && ny < G;  // :193-195
+
+  // ---- round 2: the window span and the visit rows, every load issued before any
+  // LDS write (clamped indices: unconditional loads, one memory round trip)
+  const int lo = s.x - R - 1 > 0 ? s.x - R - 1 : 0, hi = s.x + R + 1 < G - 1 ? s.x + R + 1 : G - 1;
+  const int w0 = (lo * WPR) & ~1;                      // 16-B aligned (env blocks are)
+  const int nq = ((hi + 1) * WPR - w0 + 1) >> 1;       // uint4s (a trailing pad word at most)
+  const uint4* gsrc = reinterpret_cast<const uint4*>(st.grid + e * g.gstride + w0);
+  const int vlo = s.x - 3 > 0 ? s.x - 3 : 0, vhi = s.x + 3 < G - 1 ? s.x + 3 : G - 1;
+  const int nv = (vhi - vlo + 1) * NW;
+  const uint32_t* vsrc = st.vis + e * g.vstride + (int64_t)vlo * NW;
+  uint32_t eo = 0u, en = 0u;
+  const int cell_o = s.x * G + s.y, cell_n = nx * G + (inb ? ny : s.y);
+  if (inb && (s.flags & F_EXPL_BITMAP)) {
+    eo = st.expl[e * g.estride + (cell_o >> 5)];
+    en = st.expl[e * g.estride + (cell_n >> 5)];
+  }
+  const double cthr = st.cur ? st.cur[e].thr : 0.0;  // CurriculumWrapper threshold
+  uint32_t vv[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int k = lane + 64 * j;
+    vv[j] = vsrc[k < nv ? k : nv - 1];
+  }
+  for (int q0 = 0; q0 < nq; q0 += 4 * 64) {  // one pass at G+2R <= 128 cells and 2R+3 rows <= 128
+    uint4 gv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = q0 + lane + 64 * j;
+      gv[j] = gsrc[q < nq ? q : nq - 1];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = q0 + lane + 64 * j;
+      if (q < nq) {
+        win[2 * q] = (uint64_t)gv[j].x | ((uint64_t)gv[j].y << 32);
+        win[2 * q + 1] = (uint64_t)gv[j].z | ((uint64_t)gv[j].w << 32);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int k = lane + 64 * j;
+    if (k < nv) lvis[k] = vv[j];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's LDS writes before its reads (in order)
+
+  // cell code / visit nibble from the staged window (rows outside [lo, hi] are off-map)
+  auto code_at = [&](int xr, int pcol) -> int {
+    if (xr < 0 || xr >= G) return OBST;
+    const int bit = 2 * pcol;
+    return (int)((win[xr * WPR + (bit >> 6) - w0] >> (bit & 63)) & 3u);
+  };
+  auto vword = [&](int xr, int col) -> int { return (xr - vlo) * NW + ((4 * (col + 2)) >> 5); };
+
+  // ---- transition (plantos_env.py:160-222), wave-uniform
+  s.step = s.step < 65535 ? s.step + 1 : 65535;                 // :162
+  bool ok = false, watered = false, wet_hyd = false;
+  uint32_t n = 0u;
+  double h = 0.0;
+  if (mv) {
+    ok = inb && code_at(nx, ny + R) != OBST;                     // :193-195 (plants walkable)
+    if (ok) {
+      n = (lvis[vword(nx, ny)] >> ((4 * (ny + 2)) & 31)) & 15u;
+      h = n == 0u ? rl.r_exploration : rl.r_revisit;             // :197, 204-207
+    } else {
+      s.flags |= F_COLLIDED;                                     // :209
+      s.coll = s.coll < 65535 ? s.coll + 1 : 65535;              // :210
+      h = rl.r_invalid;                                          // :211
+    }
+  } else if (water) {
+    const int cd = code_at(s.x, s.y + R);
+    if (cd == THIRSTY) {                                         // fork plantos_env_new.py:237-240
+      watered = true;
+      h = rl.r_goal;
+    } else if (cd == HYD) {                                      // fork :241-242 (root raises)
+      wet_hyd = true;
+      h = rl.r_mistake;
+    } else {
+      h = rl.r_water_empty;                                      // :221-222
+    }
+  }
+  const uint32_t nib = n < 15u ? n + 1u : 15u;                   // :203
+  uint32_t wo = eo, wn = en;
+  if (ok) {
+    if (s.flags & F_EXPL_BITMAP) {                               // explored[old]=1, [new]=2 (:198-200)
+      const uint32_t bo = 1u << (cell_o & 31), bn = 1u << (cell_n & 31);
+      if ((cell_o >> 5) == (cell_n >> 5)) {
+        if (!(wo & bo)) { wo |= bo; s.expl++; }
+        if (!(wo & bn)) { wo |= bn; s.expl++; }
+      } else {
+        if (!(wo & bo)) { wo |= bo; s.expl++; }
+        if (!(wn & bn)) { wn |= bn; s.expl++; }
+      }
+    } else if (n == 0u) {
+      s.expl++;  // derived mode: explored[new] was 0 iff never visited
+    }
+  }
+  if (bad) s.flags |= F_POISON_ACT;
+  const bool new_hyd_poison = wet_hyd && !(s.flags & F_POISON_HYD);
+  if (wet_hyd) s.flags |= F_POISON_HYD;
+  const int ox = s.x, oy = s.y;
+  if (ok) {
+    s.x = nx;                                                    // :199
+    s.y = ny;
+  }
+  double rew = rl.r_step;                                        // :164
+  rew += h;
+  bool term = s.expl >= s.total;                                 // :176, 244-246, 331
+  const bool trunc = s.step >= rl.max_steps;                     // :177
+  if (term && !(s.flags & F_BONUS)) {                            // :179-181
+    rew += rl.r_complete;
+    s.flags |= F_BONUS;
+  }
+  // the post-step window in LDS (the rays see the watered cell, the slice the visit)
+  const int kvn = ok ? vword(nx, ny) : 0;
+  const uint32_t wvn = ok ? (lvis[kvn] & ~(0xFu << ((4 * (ny + 2)) & 31))) | (nib << ((4 * (ny + 2)) & 31)) : 0u;
+  const int cbit = 2 * (oy + R), kw = ox * WPR + (cbit >> 6) - w0;
+  const uint64_t wwr = watered ? win[kw] & ~(1ull << (cbit & 63)) : 0ull;  // code 3 -> 2
+  if (lane == 0) {
+    if (bad) atomicOr(st.err_bits, F_POISON_ACT);
+    if (new_hyd_poison) atomicOr(st.err_bits, F_POISON_HYD);
+    if (st.cur) term = curriculum_hit(st.cur, e, cthr, s.expl, s.total, rl.cur_term) || term;  // A2C_training.py:101-103
+  }
+  term = __builtin_amdgcn_readfirstlane((int)term) != 0;
+  const bool done = term || trunc;
+  // an env about to be auto-reset gets new rows: its last move / watering is not
+  // stored (the terminal info accounts for the watering), unless the curriculum
+  // carries its visits over
+  const bool reset_now = done && a.autoreset;
+  const bool commit_rows = !(reset_now && !st.cur);
+  const int wfix = (watered && reset_now && !st.cur) ? 1 : 0;
+  if (lane == 0) {
+    if (ok) lvis[kvn] = wvn;
+    if (watered) win[kw] = wwr;
+    if (commit_rows) {
+      if (ok) {
+        const int b = (ny + 2) >> 1;  // the byte of the target's nibble in row nx
+        st_wt(reinterpret_cast<uint8_t*>(st.vis + e * g.vstride + (int64_t)nx * NW) + b,
+              (uint8_t)(wvn >> (8 * (b & 3))));
+        visit_bump_exact(st, g, e, cell_n, n);
+        if (s.flags & F_EXPL_BITMAP) {
+          if (wo != eo) st.expl[e * g.estride + (cell_o >> 5)] = wo;
+          if ((cell_o >> 5) != (cell_n >> 5) && wn != en) st.expl[e * g.estride + (cell_n >> 5)] = wn;
+        }
+      }
+      if (watered) {
+        const int B = (oy + R) >> 2;  // the byte of the cell's code in row ox
+        st_wt(reinterpret_cast<uint8_t*>(st.grid + e * g.gstride + (int64_t)ox * WPR) + B,
+              (uint8_t)(wwr >> (8 * (B & 7))));
+      }
+    }
+    ret += rew;
+    st_wt(a.reward + e, (float)rew);
+    st_wt(a.term + e, (uint8_t)term);
+    st_wt(a.trunc + e, (uint8_t)trunc);
+    if (done) {  // Monitor's episode return / length of the ended episode
+      if (a.ep_ret_out) st_wt(a.ep_ret_out + e, ret);
+      if (a.ep_len_out) st_wt(a.ep_len_out + e, (int32_t)s.step);
+    }
+    if (commit_rows) {  // else the reset below stores the new episode's scalars
+      st_wt(st.ep_ret + e, ret);
+      st_wt(st.scal + e, pack(s));
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+  // ---- observation (plantos_env.py:251-315) into the LDS row
+  const int xp = s.x, yp = s.y;
+  for (int i = lane; i < g.C; i += 64) {
+    const signed char* dxr = st.ldx + i * R;
+    const signed char* dyr = st.ldy + i * R;
+    int dist = R, ent = EMPTY;
+    for (int r0 = 0; r0 < R; r0 += 8) {  // offsets of 8 probes in flight, then their codes
+      int cx[8], cy[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = r0 + j < R ? r0 + j : R - 1;
+        cx[j] = xp + dxr[r];
+        cy[j] = yp + dyr[r];
+      }
+      bool hit = false;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int code = code_at(cx[j], cy[j] + R);  // :271-284 (off-map rows: obstacle)
+        if (!hit && r0 + j < R && code != EMPTY) {
+          hit = true;
+          dist = r0 + j + 1;
+          ent = code;
+        }
+      }
+      if (hit) break;
+    }
+    row[5 * i] = tab->dist[dist];                                // :288
+    row[5 * i + 1] = ent == 0 ? 1.0f : 0.0f;
+    row[5 * i + 2] = ent == 1 ? 1.0f : 0.0f;
+    row[5 * i + 3] = ent == 2 ? 1.0f : 0.0f;
+    row[5 * i + 4] = ent == 3 ? 1.0f : 0.0f;
+  }
+  if (lane < 25) {                                               // :298-313
+    const int gx = xp + lane / 5 - 2, gy = yp + lane % 5 - 2;
+    const bool in = gx >= 0 && gx < G && gy >= 0 && gy < G;
+    const uint32_t v = in ? (lvis[vword(gx, gy)] >> ((4 * (gy + 2)) & 31)) & 15u : 10u;
+    row[5 * g.C + 2 + lane] = tab->vis[v];
+  } else if (lane < 27) {
+    row[5 * g.C + lane - 25] = tab->pos[lane == 25 ? xp : yp];   // :294-296
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+  // ---- DummyVecEnv auto-reset (rare) and terminal outputs
+  if (done) {
+    if (a.tobs)
+      for (int k = lane; k < D; k += 64) a.tobs[e * D + k] = row[k];
+    if (!a.autoreset) {
+      if (a.tinfo && lane == 0) write_info(st, g, tab, e, s, a.tinfo + e * PE_NINFO);
+    } else if (a.coop_max_done > 0) {  // coop_reset_ok geometry (pe_create)
+      constexpr int KD = 6;            // D <= 347 (C <= 64): the record's obs row after its check
+      PfLoad<MAXW, KD> pl;
+      if (a.pf.scal) coop_load_prefetched<MAXW, KD>(a.pf, g, e, pl, lane);  // in flight from here on
+      bool keep = false;
+      if (st.cur && lane == 0) keep = curriculum_on_reset(st.cur, e, rl);  // A2C_training.py:56-95
+      keep = __builtin_amdgcn_readfirstlane((int)keep) != 0;
+      // with the curriculum the commit stored this env's rows: they land before the
+      // info reads them and the reset rewrites them
+      if (st.cur) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (a.tinfo) coop_write_info<MAXW>(st, g, e, s, a.tinfo + e * PE_NINFO, lane, wfix);
+      Row4<MAXW> rw;
+      Scal ns;
+      asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
+      if (a.pf.scal && coop_take_prefetched<MAXW, KD>(a.pf, g, e, s.episode, pl, rw, ns, row, lane)) {
+        ns = coop_apply_reset<MAXW>(st, g, e, ns, keep, rw, lane);
+      } else {
+        ns = coop_reset_env<MAXW>(st, g, rl, e, s.episode, keep, rw, lane, win);
+        coop_fresh_obs<MAXW>(g, rw, ns, row, tab->dist, tab->pos, tab->vis, st.ldx, st.ldy, lane);
+      }
+      if (lane == 0) {
+        if (a.pf.scal) a.pf.flag[e] = 1;  // its next map goes into the next generating batch
+        st_wt(st.ep_ret + e, 0.0);
+        st_wt(st.scal + e, pack(ns));
+      }
+    } else if (lane == 0) {  // serial reset (the geometry has no cooperative one)
+      if (a.tinfo) write_info(st, g, tab, e, s, a.tinfo + e * PE_NINFO, wfix);
+      const Scal ns = reset_env(st, g, rl, tab, e, s.episode);
+      st_wt(st.ep_ret + e, 0.0);
+      st_wt(st.scal + e, pack(ns));
+      build_obs_fresh(a, st.grid + e * g.gstride, ns, row, tab->dist, tab->pos, tab->vis, st.ldx, st.ldy);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  float* dst = a.obs + e * D;
+  for (int k = lane; k < D; k += 64) dst[k] = row[k];
+}
+
 // reset() with one wave per env (pe_coop.hpp): the map, grid/visit rows and the
 // fresh obs of env e by the 64 lanes of wave e % 4 of block e / 4 -- 65536 envs
 // are 65536 waves, so the whole chip generates maps at once (the lane-per-env
@@ -1661,7 +1923,16 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
       case V_C16R6_1W: hipLaunchKernelGGL((pe_step_fast<16, 6, true>), grid, block, lds, s, a); break;
       case V_C16R6: hipLaunchKernelGGL((pe_step_fast<16, 6, false>), grid, block, lds, s, a); break;
       case V_C64R6: hipLaunchKernelGGL((pe_step_fast<64, 6, false>), grid, block, lds, s, a); break;
-      default: hipLaunchKernelGGL(pe_step_kernel, grid, block, lds, s, a); break;
+      default: {  // pe_step_wave: one wave per env
+        const Geo& g = h->g;
+        const size_t wlds = sizeof(float) * kWaveEnvs * (size_t)wave_lds_floats(g.G, g.R, g.WPR, g.NW, g.D);
+        dim3 wgrid((unsigned)((h->n + kWaveEnvs - 1) / kWaveEnvs)), wblock(64 * kWaveEnvs);
+        if (g.WPR == 1)
+          hipLaunchKernelGGL(pe_step_wave<1>, wgrid, wblock, wlds, s, a);
+        else
+          hipLaunchKernelGGL(pe_step_wave<kCoopWPR>, wgrid, wblock, wlds, s, a);
+        break;
+      }
     }
   }
   PE_HIP(hipGetLastError());
@@ -1727,7 +1998,7 @@ const char* variant_name(int v) {
     case V_QUAD_C10R2: return "pe_step_quad<C10,R2>";
     case V_QUAD_C16R4_1W: return "pe_step_quad<C16,R4,1word>";
     case V_QUAD_C16R4: return "pe_step_quad<C16,R4>";
-    default: return "pe_step_kernel<generic>";
+    default: return "pe_step_wave";
   }
 }
 
@@ -1911,6 +2182,10 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   if (h->variant == V_QUAD_C16R6_1W && g.NW != 4) h->variant = V_C16R6_1W;  // needs 16-B visit rows
   if (is_quad(h->variant) && quad_lds_bytes(g) > 160 * 1024)
     h->variant = h->variant <= V_QUAD_C64R6 ? h->variant - (V_QUAD_C16R6_1W - V_C16R6_1W) : V_GENERIC;
+#ifdef PE_DEBUG_KNOBS
+  if (const char* kenv = std::getenv("PE_STEP_KERNEL"))
+    if (std::strcmp(kenv, "wave") == 0) h->variant = V_GENERIC;  // A/B: the one-wave-per-env kernel
+#endif
   h->kname = variant_name(h->variant);
   // explicit reset-path tuning (pe_config.coop_max_done; -1: the choice above) --
   // applied before the prefetch decision, which depends on it
@@ -1922,7 +2197,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   // which consumes no record and so queues no regeneration (20x20: 0.26 ms per
   // batch reset, against 0.09 ms for the copies + ~0.3 ms to regenerate 65536 maps).
   h->pf_every = c->prefetch_every >= 0 ? c->prefetch_every : kPrefetchEvery;
-  if (!is_quad(h->variant) || h->coop_max_done <= 0 || !c->autoreset) h->pf_every = 0;
+  if (!(is_quad(h->variant) || h->variant == V_GENERIC) || h->coop_max_done <= 0 || !c->autoreset) h->pf_every = 0;
 
   // one device allocation carved into 256-B aligned arrays
   const size_t n = (size_t)n_envs;
