@@ -628,6 +628,7 @@ __device__ __forceinline__ bool coop_take_prefetched(const Prefetch& pf, const G
                         (uint32_t)__builtin_amdgcn_readfirstlane((int)L.ps.y),
                         (uint32_t)__builtin_amdgcn_readfirstlane((int)L.ps.z), key));
   rw = L.rw;
+  if (!out) return true;  // a byte-coded record: the caller copies it (coop_copy_record_codes)
   if constexpr (PfLoad<MAXW, KD>::kEarly) {
 #pragma unroll
     for (int j = 0; j < KD; ++j)
@@ -684,15 +685,55 @@ __device__ inline Scal coop_reset_env(const State& st, const Geo& g, const Rules
   return coop_apply_reset<MAXW>(st, g, e, s, keep, rw, lane, tab);
 }
 
+// Obs writers: an obs row of f32 values (HBM or an f32 LDS tile row), or of byte
+// CODES (the byte-coded LDS obs tile of the sector kernel, pe_step_quad<..., BT>;
+// the prefetched records of such a handle).  Every obs value is one of the tables'
+// floats, so a byte names it: code c <= R+1 = dist[c] (dist[R+1] = 1.0; the
+// one-hot's 0.0 / 1.0 are codes 0 / R+1), kCodeVis + v = vis[v], kCodePos + x =
+// pos[x] (obs_code_table expands them at the tile store).
+constexpr int kCodeVis = 80, kCodePos = 96;  // R + 1 < 80, 96 + G - 1 <= 255 (G <= 128)
+
+template <typename T>
+struct ObsW;
+template <>
+struct ObsW<float> {
+  const float *tdist, *tpos, *tvis;
+  int R;
+  __device__ __forceinline__ float dist(int r) const { return tdist[r]; }
+  __device__ __forceinline__ float one(bool b) const { return b ? 1.0f : 0.0f; }
+  __device__ __forceinline__ float vis(int v) const { return tvis[v]; }
+  __device__ __forceinline__ float pos(int x) const { return tpos[x]; }
+};
+template <>
+struct ObsW<uint8_t> {
+  const float *tdist, *tpos, *tvis;  // unused
+  int R;
+  __device__ __forceinline__ uint8_t dist(int r) const { return (uint8_t)r; }
+  __device__ __forceinline__ uint8_t one(bool b) const { return b ? (uint8_t)(R + 1) : (uint8_t)0; }
+  __device__ __forceinline__ uint8_t vis(int v) const { return (uint8_t)(kCodeVis + v); }
+  __device__ __forceinline__ uint8_t pos(int x) const { return (uint8_t)(kCodePos + x); }
+};
+
+// The float of code c (one entry per thread when building the LDS code table).
+__device__ __forceinline__ float obs_code_value(const Tables* tab, int R, int G, int c) {
+  if (c <= R) return tab->dist[c];
+  if (c == R + 1) return 1.0f;
+  if (c >= kCodeVis && c < kCodeVis + 16) return tab->vis[c - kCodeVis];
+  if (c >= kCodePos && c < kCodePos + G) return tab->pos[c - kCodePos];
+  return 0.0f;
+}
+
 // build_obs_fresh by one wave from the rows in the lanes' registers: lane i
 // marches ray i (plantos_env.py:260-292), lanes 0..26 the position and the 5x5
 // slice of a fresh episode (visit 1 at the rover, :294-313).  out: the env's obs
-// row (LDS tile row or HBM); ldx/ldy: the handle's LIDAR offset tables.
-template <int MAXW>
-__device__ inline void coop_fresh_obs(const Geo& g, const Row4<MAXW>& rw, const Scal& s, float* out,
+// row (floats: LDS tile row or HBM; codes: a byte-coded tile row or record);
+// ldx/ldy: the handle's LIDAR offset tables.
+template <int MAXW, typename T = float>
+__device__ inline void coop_fresh_obs(const Geo& g, const Row4<MAXW>& rw, const Scal& s, T* out,
                                       const float* tdist, const float* tpos, const float* tvis,
                                       const signed char* ldx, const signed char* ldy, int lane) {
   const int R = g.R, C = g.C, G = g.G;
+  const ObsW<T> w{tdist, tpos, tvis, R};
   // every lane takes part in every row fetch (a lane that left the loop could not
   // serve its row to the others): first hits are latched, not broken out of
   const int li = lane < C ? lane : 0;
@@ -706,8 +747,8 @@ __device__ inline void coop_fresh_obs(const Geo& g, const Row4<MAXW>& rw, const 
     const int bit = 2 * (cy + R);
     Row4<MAXW> fetched{0ull, 0ull, 0ull, 0ull};
 #pragma unroll
-    for (int w = 0; w < MAXW; ++w)
-      if (MAXW == 1 || w < g.WPR) fetched.set(w, shfl64(rw.get(w), src));
+    for (int k = 0; k < MAXW; ++k)
+      if (MAXW == 1 || k < g.WPR) fetched.set(k, shfl64(rw.get(k), src));
     const uint64_t word = fetched.get(bit >> 6);
     const int code = inr ? (int)((word >> (bit & 63)) & 3u) : OBST;  // :271-284
     if (!hit && code != EMPTY) {
@@ -717,21 +758,29 @@ __device__ inline void coop_fresh_obs(const Geo& g, const Row4<MAXW>& rw, const 
     }
   }
   if (lane < C) {
-    out[5 * lane] = tdist[dist];
-    out[5 * lane + 1] = ent == 0 ? 1.0f : 0.0f;
-    out[5 * lane + 2] = ent == 1 ? 1.0f : 0.0f;
-    out[5 * lane + 3] = ent == 2 ? 1.0f : 0.0f;
-    out[5 * lane + 4] = ent == 3 ? 1.0f : 0.0f;
+    out[5 * lane] = w.dist(dist);
+    out[5 * lane + 1] = w.one(ent == 0);
+    out[5 * lane + 2] = w.one(ent == 1);
+    out[5 * lane + 3] = w.one(ent == 2);
+    out[5 * lane + 4] = w.one(ent == 3);
   }
   if (lane < 25) {
     const int lx = lane / 5, ly = lane % 5;
     const int gx = s.x + lx - 2, gy = s.y + ly - 2;
     const bool in = gx >= 0 && gx < G && gy >= 0 && gy < G;  // :307-311
     const bool rover = lane == 12 && !(s.flags & F_NOROOM);
-    out[5 * C + 2 + lane] = !in ? tvis[10] : (rover ? tvis[1] : tvis[0]);
+    out[5 * C + 2 + lane] = w.vis(!in ? 10 : (rover ? 1 : 0));
   } else if (lane < 27) {
-    out[5 * C + lane - 25] = tpos[lane == 25 ? s.x : s.y];  // :294-296
+    out[5 * C + lane - 25] = w.pos(lane == 25 ? s.x : s.y);  // :294-296
   }
+}
+
+// The prefetched record's obs row as codes (a byte-coded handle: pf.obs holds D
+// bytes per env) copied into a byte-coded tile row, once the record is taken.
+__device__ __forceinline__ void coop_copy_record_codes(const Prefetch& pf, const Geo& g, int64_t e, uint8_t* out,
+                                                       int lane) {
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(pf.obs) + e * g.D;
+  for (int k = lane; k < g.D; k += 64) out[k] = src[k];
 }
 
 }  // namespace pe

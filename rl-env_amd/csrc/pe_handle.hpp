@@ -14,6 +14,8 @@ struct pe_handle {
   void* mem;
   size_t bytes;
   int variant;
+  int tile_codes;    // the sector kernel's obs tile holds byte codes (pe_step_quad<..., BT>); so do the
+                     // prefetched records' obs rows
   const char* kname;
   void* cur_mem;     // CurriculumWrapper records (pe_curriculum_enable), or NULL
   size_t lds_floor;  // minimum dynamic LDS per step workgroup (PE_LDS_FLOOR, debug builds only)

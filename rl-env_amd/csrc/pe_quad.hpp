@@ -24,6 +24,7 @@
 #pragma once
 #include <type_traits>
 
+#include "pe_coop.hpp"
 #include "pe_device.hpp"
 
 namespace pe {
@@ -73,8 +74,9 @@ constexpr int kOneHotF = 48;
 // one find-first-set over their nonzero bits (a sentinel at bit 2R: nothing hit,
 // range R, entity EMPTY), and its distance and one-hot come from LDS tables:
 // ~3 VALU per probe instead of a compare-and-select chain per probe and per float.
-template <int C, int R, int NW, int W>
-__device__ __forceinline__ void quad_rays(const uint64_t* lrow, int lane, int kc, int sh, bool watered, float* row,
+// OT: float (an f32 tile row) or uint8_t (a byte-coded tile row, pe_coop.hpp ObsW).
+template <int C, int R, int NW, int W, typename OT>
+__device__ __forceinline__ void quad_rays(const uint64_t* lrow, int lane, int kc, int sh, bool watered, OT* row,
                                           const float* tdist) {
   constexpr int I0 = W * C / NW, I1 = (W + 1) * C / NW;
   constexpr int LO = ray_dx_min<C, R>(I0, I1), HI = ray_dx_max<C, R>(I0, I1);
@@ -102,35 +104,50 @@ __device__ __forceinline__ void quad_rays(const uint64_t* lrow, int lane, int kc
     const uint32_t nz = ((pk | (pk >> 1)) & kNZ) | (1u << (2 * R));
     const int f = __builtin_ctz(nz);         // 2(r-1) of the first hit, 2R if none
     const int ent = (int)((pk >> f) & 3u);   // its code (EMPTY if none)
-    row[5 * i] = tdist[(f >> 1) + 1];        // float(r / R), plantos_env.py:288 (R/R if none)
-    const float4 oh = tone[ent];
-    row[5 * i + 1] = oh.x;
-    row[5 * i + 2] = oh.y;
-    row[5 * i + 3] = oh.z;
-    row[5 * i + 4] = oh.w;
+    if constexpr (std::is_same<OT, float>::value) {
+      row[5 * i] = tdist[(f >> 1) + 1];      // float(r / R), plantos_env.py:288 (R/R if none)
+      const float4 oh = tone[ent];
+      row[5 * i + 1] = oh.x;
+      row[5 * i + 2] = oh.y;
+      row[5 * i + 3] = oh.z;
+      row[5 * i + 4] = oh.w;
+    } else {
+      row[5 * i] = (uint8_t)((f >> 1) + 1);  // code r = dist[r] (R+1: 1.0, nothing hit)
+      const uint32_t oh = (uint32_t)(R + 1) << (8 * ent);  // one-hot as codes {0, R+1}
+      row[5 * i + 1] = (uint8_t)oh;
+      row[5 * i + 2] = (uint8_t)(oh >> 8);
+      row[5 * i + 3] = (uint8_t)(oh >> 16);
+      row[5 * i + 4] = (uint8_t)(oh >> 24);
+    }
   }
 }
 
 // Wave-uniform dispatch of the sector code (wv comes from readfirstlane).
-template <int C, int R, int NW, int W = 0>
+template <int C, int R, int NW, int W = 0, typename T>
 __device__ __forceinline__ void sector_rays(int wv, const uint64_t* lrow, int lane, int kc, int sh, bool watered,
-                                            float* row, const float* tdist) {
+                                            T* row, const float* tdist) {
   if constexpr (W < NW) {
     if (wv == W)
-      quad_rays<C, R, NW, W>(lrow, lane, kc, sh, watered, row, tdist);
+      quad_rays<C, R, NW, W, T>(lrow, lane, kc, sh, watered, row, tdist);
     else
-      sector_rays<C, R, NW, W + 1>(wv, lrow, lane, kc, sh, watered, row, tdist);
+      sector_rays<C, R, NW, W + 1, T>(wv, lrow, lane, kc, sh, watered, row, tdist);
   }
 }
 
 // One row lx of the 5x5 visit slice (plantos_env.py:298-313) from the LDS visit
 // rows (row k = visit row x-3+k, 8 nibbles from padded column ybv).
+template <typename T>
 __device__ __forceinline__ void quad_slice_row(const uint32_t* lvis, int lane, int lx, int dxv, int vs, bool bump,
-                                               uint32_t nib, int C, float* row, const float* tvis) {
+                                               uint32_t nib, int C, T* row, const float* tvis) {
   uint32_t v = lvis[(dxv + 1 + lx) * kQuadEnvs + lane] >> vs;
   if (lx == 2 && bump) v = (v & ~0xF00u) | (nib << 8);  // the move's own visit (:203)
 #pragma unroll
-  for (int ly = 0; ly < 5; ++ly) row[5 * C + 2 + 5 * lx + ly] = tvis[(v >> (4 * ly)) & 15u];
+  for (int ly = 0; ly < 5; ++ly) {
+    if constexpr (std::is_same<T, float>::value)
+      row[5 * C + 2 + 5 * lx + ly] = tvis[(v >> (4 * ly)) & 15u];
+    else
+      row[5 * C + 2 + 5 * lx + ly] = (uint8_t)(kCodeVis + ((v >> (4 * ly)) & 15u));
+  }
 }
 
 }  // namespace pe

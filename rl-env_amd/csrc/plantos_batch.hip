@@ -266,6 +266,36 @@ __device__ __forceinline__ void store_tile(const float* rows, float* dst, int va
   }
 }
 
+// Stream the block's byte-coded [valid x D] obs tile (contiguous codes, pe_coop.hpp
+// ObsW<uint8_t>) to HBM as floats: 4 codes per thread and step expanded through the
+// LDS code table ctab[256] into one 16-B store (same store policy as store_tile).
+__device__ __forceinline__ void store_tile_codes(const uint8_t* codes, const float* ctab, float* dst, int valid, int D,
+                                                 int t0, int nt) {
+  const int total = valid * D;
+  if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+    const int n4 = total >> 2;
+    const uint32_t* c4 = reinterpret_cast<const uint32_t*>(codes);
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    v4f* d4 = reinterpret_cast<v4f*>(dst);
+    for (int k = t0; k < n4; k += nt) {
+      const uint32_t c = c4[k];
+      v4f v;
+      v.x = ctab[c & 255u];
+      v.y = ctab[(c >> 8) & 255u];
+      v.z = ctab[(c >> 16) & 255u];
+      v.w = ctab[c >> 24];
+#if defined(PE_OBS_STORE_ASM)
+      asm volatile("global_store_dwordx4 %0, %1, off " PE_OBS_STORE_ASM "\n\ts_nop 1" ::"v"(d4 + k), "v"(v) : "memory");
+#else
+      d4[k] = v;
+#endif
+    }
+    for (int k = (n4 << 2) + t0; k < total; k += nt) dst[k] = ctab[codes[k]];
+  } else {
+    for (int k = t0; k < total; k += nt) dst[k] = ctab[codes[k]];
+  }
+}
+
 // ------------------------------------------------------------------ kernels
 // Specialized fused step (compile-time C, R): two load rounds per lane, the rest
 // from registers (pe_fast.hpp).  Same semantics as pe_step_wave.
@@ -496,6 +526,11 @@ template <int R>
 constexpr int quad_tile_off() {
   return (kTabFloats + (2 * R + 3) * kQuadEnvs * 2 + 7 * kQuadEnvs + 3) & ~3;
 }
+// byte-coded tile (BT): the code table ctab[256] after the [64 x D] code tile
+template <int R, int C>
+constexpr int quad_ctab_off() {
+  return quad_tile_off<R>() + ((kQuadEnvs * (5 * C + 27) + 15) / 16) * 4;
+}
 
 // ---- pe_step_quad's auto-reset slow path (a block with a done env), out of line:
 // kept in separate functions so that their register demand (map generation, the
@@ -515,9 +550,11 @@ __device__ __forceinline__ bool quad_coop(const StepArgs& a, int ndone) {
 #endif
 }
 
-template <int NW, bool ONEWORD, int KD>  // one copy per kernel: each inherits its kernel's register budget
+// BT: the obs tile holds byte codes (ctab: the LDS code table), see pe_step_quad.
+template <int NW, bool ONEWORD, int KD, bool BT = false>  // one copy per kernel: each inherits its kernel's register budget
 __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, int C, int R, int lane, int wv, int CW,
-                                                int64_t e0, bool done, uint4 sp, double ret, int ndone, bool wfix) {
+                                                int64_t e0, bool done, uint4 sp, double ret, int ndone, bool wfix,
+                                                const float* ctab = nullptr) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const StepArgs& a = *reinterpret_cast<const StepArgs*>(ka);
   const Geo& g = a.g;
@@ -528,11 +565,27 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
   float* tvis = smem + 328;
   const Tables* ltab = reinterpret_cast<const Tables*>(smem);
   uint64_t* lrow = reinterpret_cast<uint64_t*>(smem + kTabFloats);
-  float* rows = smem + tile_off;
-  float* row = rows + lane * g.D;
+  using OT = typename std::conditional<BT, uint8_t, float>::type;
+  OT* rows = reinterpret_cast<OT*>(smem + tile_off);
+  OT* row = rows + lane * g.D;
   const int64_t e = e0 + lane;
   Scal s = unpack(sp);
   constexpr int MAXW = ONEWORD ? 1 : kCoopWPR;
+  // an obs tile value as a float (BT: expand the code)
+  auto tval = [&](const OT* r, int k) -> float {
+    if constexpr (BT) return ctab[r[k]];
+    else return r[k];
+  };
+  // a prefetched record's fresh obs row into tile row `o` once taken (BT: codes)
+  auto take = [&](int64_t el, uint32_t episode, const PfLoad<MAXW, KD>& pl, Row4<MAXW>& rw, Scal& ns, OT* o) -> bool {
+    if constexpr (BT) {
+      if (!coop_take_prefetched<MAXW, KD>(a.pf, g, el, episode, pl, rw, ns, nullptr, lane)) return false;
+      coop_copy_record_codes(a.pf, g, el, o, lane);
+      return true;
+    } else {
+      return coop_take_prefetched<MAXW, KD>(a.pf, g, el, episode, pl, rw, ns, o, lane);
+    }
+  };
   if (ndone == 1 && quad_coop(a, ndone)) {
     // One done env (the usual case with desynchronized episodes): the commit wave,
     // which holds its scalars, resets it alone -- no staging, one barrier.
@@ -541,7 +594,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
       const uint64_t dmw = reinterpret_cast<const uint64_t*>(smem)[35];
       const int l = __ffsll((unsigned long long)dmw) - 1;
       const int64_t el = e0 + l;
-      float* orow = rows + l * g.D;
+      OT* orow = rows + l * g.D;
       PfLoad<MAXW, KD> pl;
       if (a.pf.scal) coop_load_prefetched<MAXW, KD>(a.pf, g, el, pl, lane);  // in flight from here on
       bool keep = false;
@@ -554,7 +607,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
                                         (uint32_t)__builtin_amdgcn_readlane((int)sp.w, l)));
       if (a.tobs) {
         float* t = a.tobs + el * g.D;
-        for (int k2 = lane; k2 < g.D; k2 += 64) t[k2] = orow[k2];
+        for (int k2 = lane; k2 < g.D; k2 += 64) t[k2] = tval(orow, k2);
       }
       // with the curriculum the commit stored this env's rows: they must land before
       // the info reads them and the reset rewrites them
@@ -565,7 +618,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
       Row4<MAXW> rw;
       Scal ns;
       asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
-      if (a.pf.scal && coop_take_prefetched<MAXW, KD>(a.pf, g, el, sv.episode, pl, rw, ns, orow, lane)) {
+      if (a.pf.scal && take(el, sv.episode, pl, rw, ns, orow)) {
         ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane);
       } else {
         uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
@@ -625,10 +678,10 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         dm &= dm - 1;
         if (k % NWv != wv) continue;
         const int64_t el = e0 + l;
-        float* orow = rows + l * g.D;
+        OT* orow = rows + l * g.D;
         if (a.tobs) {
           float* t = a.tobs + el * g.D;
-          for (int k2 = lane; k2 < g.D; k2 += 64) t[k2] = orow[k2];
+          for (int k2 = lane; k2 < g.D; k2 += 64) t[k2] = tval(orow, k2);
         }
         const uint4 sl = make_uint4((uint32_t)__builtin_amdgcn_readfirstlane((int)stage[5 * l]),
                                     (uint32_t)__builtin_amdgcn_readfirstlane((int)stage[5 * l + 1]),
@@ -644,7 +697,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         Row4<MAXW> rw;
         Scal ns;
         asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
-        if (a.pf.scal && coop_take_prefetched<MAXW, KD>(a.pf, g, el, sv.episode, pl, rw, ns, orow, lane)) {
+        if (a.pf.scal && take(el, sv.episode, pl, rw, ns, orow)) {
           ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane);
         } else {
           uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
@@ -679,9 +732,11 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
   // the new map is generated there when it can hold the grid image (LDS latency
   // for the rejection-sampling scans; the fresh obs row goes straight to HBM
   // after the tile store, quad_done_obs)
-  const bool scratch_ok = reset_scratch_bytes(g.G, g.WPR, rl.P) <= 4 * g.D;
+  // (BT: the tile row holds D bytes, never the image; the fresh obs of that case is
+  // built from the env's grid in HBM after the tile store, quad_done_obs)
+  const bool scratch_ok = !BT && reset_scratch_bytes(g.G, g.WPR, rl.P) <= 4 * g.D;
   // 8-B aligned start inside the row (rows is 16-B aligned, D is odd)
-  uint64_t* sg = reinterpret_cast<uint64_t*>(row + ((lane * g.D) & 1));
+  uint64_t* sg = reinterpret_cast<uint64_t*>(reinterpret_cast<float*>(rows) + lane * g.D + ((lane * g.D) & 1));
   // LIDAR offsets for the reset-path obs builders, staged in the (now dead) window region
   const signed char* lldx = reinterpret_cast<const signed char*>(lrow);
   const signed char* lldy = lldx + C * R;
@@ -695,7 +750,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
   if (done) {
     if (a.tobs) {
       float* t = a.tobs + e * g.D;
-      for (int k = 0; k < g.D; ++k) t[k] = row[k];
+      for (int k = 0; k < g.D; ++k) t[k] = tval(row, k);
     }
     PE_RSTAMP(1);
     if (a.tinfo) write_info(a.st, a.g, ltab, e, s, a.tinfo + e * PE_NINFO, wfix);
@@ -706,7 +761,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
       PE_RSTAMP(3);
     } else {
       s = reset_env(st, g, rl, ltab, e, s.episode);
-      build_obs_fresh(a, st.grid + e * g.gstride, s, row, tdist, tpos, tvis, lldx, lldy);
+      if constexpr (!BT) build_obs_fresh(a, st.grid + e * g.gstride, s, row, tdist, tpos, tvis, lldx, lldy);
     }
     if (a.autoreset) {
       st.ep_ret[e] = 0.0;
@@ -718,20 +773,24 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
 }
 
 // The lane-per-env path's fresh obs, after the tile store (see quad_done_path).
-template <int NW>
+template <int NW, bool BT = false>
 __device__ __forceinline__ void quad_done_obs(const void* ka, int tile_off, int lane, int64_t e, bool done, uint4 sp) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const StepArgs& a = *reinterpret_cast<const StepArgs*>(ka);
   const Geo& g = a.g;
   float* row = smem + tile_off + lane * g.D;
-  const uint64_t* sg = reinterpret_cast<const uint64_t*>(row + ((lane * g.D) & 1));
+  // the grid image: the LDS scratch in the env's tile row, or (BT) the env's rows in HBM
+  const uint64_t* sg = BT ? a.st.grid + e * g.gstride : reinterpret_cast<const uint64_t*>(row + ((lane * g.D) & 1));
   const signed char* lldx = reinterpret_cast<const signed char*>(smem + kTabFloats);
   PE_RSTAMP(4);
   if (done) build_obs_fresh(a, sg, unpack(sp), a.obs + e * g.D, smem, smem + 72, smem + 328, lldx, lldx + g.C * g.R);
   PE_RSTAMP(5);
 }
 
-template <int C, int R, bool ONEWORD, int NW>
+// BT: byte-coded obs tile (pe_coop.hpp ObsW<uint8_t>): [64 x D] bytes instead of
+// floats in LDS (64x64 / 64 rays: 22 KB instead of 89 KB), expanded through the LDS
+// code table at the tile store -- the f32 tile held the kernel to one workgroup per CU.
+template <int C, int R, bool ONEWORD, int NW, bool BT = false>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs; NW=4: <= 128 VGPRs (4 workgroups per CU: G=25 13.1 -> 10.5 us; 1-word C16: 122 -> 104 VGPRs)
   constexpr int NR = 2 * R + 3, NV = 7, EPB = kQuadEnvs, CW = NW - 1;  // CW: commit wave
 
@@ -744,7 +803,9 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   float* tvis = smem + 328;
   uint64_t* lrow = reinterpret_cast<uint64_t*>(smem + kTabFloats);  // [NR][EPB]
   uint32_t* lvis = reinterpret_cast<uint32_t*>(lrow + NR * EPB);    // [NV][EPB]
-  float* rows = smem + quad_tile_off<R>();                          // [EPB][D]
+  using OT = typename std::conditional<BT, uint8_t, float>::type;
+  OT* rows = reinterpret_cast<OT*>(smem + quad_tile_off<R>());     // [EPB][D] floats or codes
+  float* ctab = smem + quad_ctab_off<R, C>();                       // BT: code -> float
   const Geo& g = a.g;
   const Rules& rl = a.rl;
   const State& st = a.st;
@@ -791,6 +852,9 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   static_assert(R + 2 <= kOneHotF && kOneHotF + 16 <= 70, "ray tables inside dist[], below the done mask");
   if (threadIdx.x < 16) smem[kOneHotF + threadIdx.x] = (threadIdx.x >> 2) == (threadIdx.x & 3) ? 1.0f : 0.0f;
   if (threadIdx.x == 16) smem[R + 1] = 1.0f;
+  if constexpr (BT) {
+    if (threadIdx.x < 256) ctab[threadIdx.x] = obs_code_value(st.tab, R, g.G, (int)threadIdx.x);
+  }
   const Tables* ltab = reinterpret_cast<const Tables*>(smem);
   Scal s = unpack(sw);
 #ifdef PE_STAMPS
@@ -991,7 +1055,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   }
   const int xp = s.x + dxv, yp = ok ? ny : s.y;
   const uint32_t nib = n < 15u ? n + 1u : 15u;                    // :203
-  float* row = rows + lane * g.D;
+  OT* row = rows + lane * g.D;
   bool done = false, wfix = false;
   if (live) {
     const int kc = dxv + R + 1;
@@ -1001,9 +1065,14 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
     // slice rows and position go to the non-commit waves (the commit wave is the laggard)
     if (wv != CW)
       for (int lx = wv; lx < 5; lx += NW - 1) quad_slice_row(lvis, lane, lx, dxv, vs, ok, nib, C, row, tvis);
-    if (wv == (NW == 4 ? 2 : 5)) {
-      row[5 * C] = tpos[xp];                                      // :294-296
-      row[5 * C + 1] = tpos[yp];
+    if (wv == (NW == 4 ? 2 : 5)) {                                // :294-296
+      if constexpr (BT) {
+        row[5 * C] = (uint8_t)(kCodePos + xp);
+        row[5 * C + 1] = (uint8_t)(kCodePos + yp);
+      } else {
+        row[5 * C] = tpos[xp];
+        row[5 * C + 1] = tpos[yp];
+      }
     }
     if (wv == CW && !(kAblate & 8)) {
       // ---- commit (plantos_env.py:160-222)
@@ -1120,8 +1189,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   static_assert(5 * 4 * EPB + 8 <= (NR * 8 + NV * 4) * EPB, "reset staging must fit the window region");
   const int64_t valid = a.n - e0 < EPB ? a.n - e0 : EPB;
   if (__builtin_expect(any_done, 0)) {  // cold: laid out after the hot path
-    const uint4 ns = quad_done_path<NW, ONEWORD, (5 * C + 27 + 63) / 64>(kernargs(), quad_tile_off<R>(), C, R, lane, wv,
-                                                                       CW, e0, done, pack(s), ret, ndone, wfix);
+    const uint4 ns = quad_done_path<NW, ONEWORD, (5 * C + 27 + 63) / 64, BT>(
+        kernargs(), quad_tile_off<R>(), C, R, lane, wv, CW, e0, done, pack(s), ret, ndone, wfix, ctab);
     s = unpack(ns);
   }
   // the obs tile goes out through the waves other than the commit wave: its state
@@ -1131,17 +1200,26 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   if constexpr (!(kAblate & 1)) {
     if constexpr (C >= 64) {  // long rows: the commit wave's share pays for its wait (64x64: 33.2 -> 32.7 us)
       if (wv == CW) __builtin_amdgcn_s_waitcnt(0x0F70);  // tracked vmcnt(0): no wait inside the loop
-      store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D);
+      if constexpr (BT)
+        store_tile_codes(rows, ctab, a.obs + e0 * g.D, (int)valid, g.D, (int)threadIdx.x, (int)blockDim.x);
+      else
+        store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D);
     } else {
-      if (wv != CW) store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D, (int)threadIdx.x, 64 * (NW - 1));
+      if (wv != CW) {
+        if constexpr (BT)
+          store_tile_codes(rows, ctab, a.obs + e0 * g.D, (int)valid, g.D, (int)threadIdx.x, 64 * (NW - 1));
+        else
+          store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D, (int)threadIdx.x, 64 * (NW - 1));
+      }
     }
   }
-  if (any_done && a.autoreset && !quad_coop(a, ndone) && reset_scratch_bytes(g.G, g.WPR, rl.P) <= 4 * g.D) {
-    // the tile store above wrote scratch bytes into the done rows: drain it, then
-    // overwrite those rows with the fresh obs built from the LDS grid image
+  if (any_done && a.autoreset && !quad_coop(a, ndone) && (BT || reset_scratch_bytes(g.G, g.WPR, rl.P) <= 4 * g.D)) {
+    // the tile store above wrote stale values (scratch bytes / the terminal codes)
+    // into the done rows: drain it, then overwrite those rows with the fresh obs built
+    // from the grid image (LDS scratch, or BT: the env's rows in HBM)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    quad_done_obs<NW>(kernargs(), quad_tile_off<R>(), lane, e, done, pack(s));
+    quad_done_obs<NW, BT>(kernargs(), quad_tile_off<R>(), lane, e, done, pack(s));
   }
   PE_STAMP(6);
 #ifdef PE_STAMPS
@@ -1523,7 +1601,7 @@ __global__ __launch_bounds__(256) void pe_pf_compact_kernel(Prefetch pf, int n) 
 // over the queue, then the last workgroup clears the queue), or of every env
 // (all != 0: one wave per env; after create / reset()), skipping envs whose
 // record already holds the reset of their current episode counter.
-template <int MAXW>
+template <int MAXW, bool BT = false>  // BT: the records' obs rows as byte codes (a byte-coded step tile)
 __global__ __launch_bounds__(256) void pe_prefetch_kernel(StepArgs a, int all) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const Geo& g = a.g;
@@ -1548,7 +1626,11 @@ __global__ __launch_bounds__(256) void pe_prefetch_kernel(StepArgs a, int all) {
       for (int w = 0; w < MAXW; ++w)
         if (MAXW == 1 || w < g.WPR) dst[w] = rw.get(w);
     }
-    coop_fresh_obs<MAXW>(g, rw, s, pf.obs + e * g.D, smem, smem + 72, smem + 328, a.st.ldx, a.st.ldy, lane);
+    if constexpr (BT)
+      coop_fresh_obs<MAXW>(g, rw, s, reinterpret_cast<uint8_t*>(pf.obs) + e * g.D, smem, smem + 72, smem + 328,
+                           a.st.ldx, a.st.ldy, lane);
+    else
+      coop_fresh_obs<MAXW>(g, rw, s, pf.obs + e * g.D, smem, smem + 72, smem + 328, a.st.ldx, a.st.ldy, lane);
     if (lane == 0) pf.scal[e] = pack(s);  // read by a later launch only
   }
   if (!all) {
@@ -1886,9 +1968,11 @@ enum Variant {
   V_QUAD_C16R4_1W = 9, V_QUAD_C16R4 = 10  // test_environment.py:24 (G=15, C=16, R=4)
 };
 
-size_t quad_lds_bytes(const Geo& g) {
-  return sizeof(float) * ((size_t)((kTabFloats + (2 * g.R + 3) * kQuadEnvs * 2 + 7 * kQuadEnvs + 3) & ~3) +
-                          (size_t)kQuadEnvs * g.D);
+size_t quad_lds_bytes(const Geo& g, bool codes) {
+  const size_t off = (size_t)((kTabFloats + (2 * g.R + 3) * kQuadEnvs * 2 + 7 * kQuadEnvs + 3) & ~3);
+  if (codes)  // byte tile + code table (quad_ctab_off)
+    return sizeof(float) * (off + (size_t)((kQuadEnvs * g.D + 15) / 16) * 4 + 256);
+  return sizeof(float) * (off + (size_t)kQuadEnvs * g.D);
 }
 
 bool is_quad(int v) { return v >= V_QUAD_C16R6_1W; }
@@ -1897,17 +1981,19 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
   if (is_quad(h->variant)) {
     const int nw = h->quad_waves;
     dim3 grid((unsigned)((h->n + kQuadEnvs - 1) / kQuadEnvs)), block(nw * 64);
-    size_t lds = quad_lds_bytes(h->g);
+    size_t lds = quad_lds_bytes(h->g, h->tile_codes);
     if (h->lds_floor > lds) lds = h->lds_floor;  // diagnostics: caps workgroups per CU
 #define PE_QUAD(CC, RR, OW)                                                                 \
-  if (nw == 8)                                                                              \
+  if (h->tile_codes)                                                                        \
+    hipLaunchKernelGGL((pe_step_quad<CC, RR, OW, 4, true>), grid, block, lds, s, a);        \
+  else if (nw == 8)                                                                         \
     hipLaunchKernelGGL((pe_step_quad<CC, RR, OW, 8>), grid, block, lds, s, a);              \
   else                                                                                      \
     hipLaunchKernelGGL((pe_step_quad<CC, RR, OW, 4>), grid, block, lds, s, a);
 #define PE_QUAD4(CC, RR, OW) hipLaunchKernelGGL((pe_step_quad<CC, RR, OW, 4>), grid, block, lds, s, a);
     switch (h->variant) {
       case V_QUAD_C16R6_1W: PE_QUAD(16, 6, true); break;
-      case V_QUAD_C16R6: PE_QUAD(16, 6, false); break;
+      case V_QUAD_C16R6: PE_QUAD4(16, 6, false); break;
       case V_QUAD_C64R6: PE_QUAD(64, 6, false); break;
       case V_QUAD_C10R2_1W: PE_QUAD4(10, 2, true); break;
       case V_QUAD_C10R2: PE_QUAD4(10, 2, false); break;
@@ -1952,10 +2038,17 @@ int launch_prefetch(const pe_handle* h, hipStream_t s, int all) {
     PE_HIP(hipGetLastError());
   }
   const size_t lds = sizeof(float) * (size_t)kTabFloats + 4 * 8 * (size_t)coop_scratch_words(h->g.G, h->g.WPR);
-  if (h->g.WPR == 1)
-    hipLaunchKernelGGL(pe_prefetch_kernel<1>, grid, block, lds, s, a, all);
-  else
-    hipLaunchKernelGGL(pe_prefetch_kernel<kCoopWPR>, grid, block, lds, s, a, all);
+  if (h->g.WPR == 1) {
+    if (h->tile_codes)
+      hipLaunchKernelGGL((pe_prefetch_kernel<1, true>), grid, block, lds, s, a, all);
+    else
+      hipLaunchKernelGGL((pe_prefetch_kernel<1, false>), grid, block, lds, s, a, all);
+  } else {
+    if (h->tile_codes)
+      hipLaunchKernelGGL((pe_prefetch_kernel<kCoopWPR, true>), grid, block, lds, s, a, all);
+    else
+      hipLaunchKernelGGL((pe_prefetch_kernel<kCoopWPR, false>), grid, block, lds, s, a, all);
+  }
   PE_HIP(hipGetLastError());
   return PE_OK;
 }
@@ -2180,12 +2273,21 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   const bool oneword = g.WPR == 1 && g.NW == 4;
   if ((h->variant == V_QUAD_C10R2_1W || h->variant == V_QUAD_C16R4_1W) && !oneword) h->variant += 1;
   if (h->variant == V_QUAD_C16R6_1W && g.NW != 4) h->variant = V_C16R6_1W;  // needs 16-B visit rows
-  if (is_quad(h->variant) && quad_lds_bytes(g) > 160 * 1024)
+  // byte-coded obs tile where the f32 tile limits the sector kernel's occupancy
+  // (C = 64: 89 KB -> 22 KB of LDS per workgroup)
+  h->tile_codes = h->variant == V_QUAD_C64R6 ? 1 : 0;
+#ifdef PE_DEBUG_KNOBS
+  if (const char* tc = std::getenv("PE_TILE_CODES"))
+    if (h->variant == V_QUAD_C16R6_1W || h->variant == V_QUAD_C64R6) h->tile_codes = std::atoi(tc) != 0;
+#endif
+  if (h->tile_codes) h->quad_waves = 4;
+  if (is_quad(h->variant) && quad_lds_bytes(g, h->tile_codes) > 160 * 1024)
     h->variant = h->variant <= V_QUAD_C64R6 ? h->variant - (V_QUAD_C16R6_1W - V_C16R6_1W) : V_GENERIC;
 #ifdef PE_DEBUG_KNOBS
   if (const char* kenv = std::getenv("PE_STEP_KERNEL"))
     if (std::strcmp(kenv, "wave") == 0) h->variant = V_GENERIC;  // A/B: the one-wave-per-env kernel
 #endif
+  if (!is_quad(h->variant)) h->tile_codes = 0;
   h->kname = variant_name(h->variant);
   // explicit reset-path tuning (pe_config.coop_max_done; -1: the choice above) --
   // applied before the prefetch decision, which depends on it
@@ -2264,8 +2366,8 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
     const size_t plds = sizeof(float) * (size_t)kTabFloats + 4 * 8 * (size_t)coop_scratch_words(G, g.WPR);
     int per_cu = 0;
     hipError_t oe = g.WPR == 1
-        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pe_prefetch_kernel<1>, 256, plds)
-        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pe_prefetch_kernel<kCoopWPR>, 256, plds);
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pe_prefetch_kernel<1, false>, 256, plds)
+        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pe_prefetch_kernel<kCoopWPR, false>, 256, plds);
     if (oe != hipSuccess || per_cu < 1) per_cu = 1;
     h->pf_blocks = per_cu * prop.multiProcessorCount;
   }
