@@ -1250,7 +1250,11 @@ __host__ __device__ constexpr int wave_win_words(int G, int R, int WPR) {
 __host__ __device__ constexpr int wave_lds_floats(int G, int R, int WPR, int NW, int D) {
   return 2 * wave_win_words(G, R, WPR) + ((7 * NW + 3) & ~3) + ((D + 3) & ~3);
 }
-constexpr int kWaveEnvs = 4;  // envs (waves) per workgroup
+// The workgroup's shared header: the obs tables (Tables' first 344 floats: dist,
+// pos, vis) and the LIDAR offsets as int16 (dx & 0xFF | dy << 8) [C][RP], RP = R
+// rounded up to 8 (one 16-B LDS read per 8 probes of a ray).
+__host__ __device__ constexpr int wave_hdr_floats(int C, int R) { return 344 + C * ((R + 7) & ~7) / 2; }
+constexpr int kWaveEnvs = 8;  // envs (waves) per workgroup
 
 template <int MAXW>  // the cooperative reset's row words (1 or kCoopWPR)
 __global__ __launch_bounds__(64 * kWaveEnvs) void pe_step_wave(StepArgs a) {
@@ -1258,13 +1262,25 @@ __global__ __launch_bounds__(64 * kWaveEnvs) void pe_step_wave(StepArgs a) {
   const Geo& g = a.g;
   const Rules& rl = a.rl;
   const State& st = a.st;
-  const Tables* tab = st.tab;  // global (L1/L2-resident): 4 envs per workgroup would re-load an LDS copy per 4 envs
+  const Tables* tab = st.tab;  // global: the serial reset path's tables
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int64_t e = (int64_t)blockIdx.x * kWaveEnvs + wv;
+  const int G = g.G, R = g.R, WPR = g.WPR, NW = g.NW, D = g.D, RP = (R + 7) & ~7;
+  // the shared header (its loads overlap round 1 below; read after the barrier)
+  const float* tsrc = reinterpret_cast<const float*>(tab);
+  for (int k = threadIdx.x; k < 344; k += blockDim.x) smem[k] = tsrc[k];
+  int16_t* lofs = reinterpret_cast<int16_t*>(smem + 344);
+  for (int k = threadIdx.x; k < g.C * RP; k += blockDim.x) {
+    const int i = k / RP, r = k - i * RP;
+    lofs[k] = r < R ? (int16_t)((uint8_t)st.ldx[i * R + r] | ((int)st.ldy[i * R + r] << 8)) : (int16_t)0;
+  }
+  __syncthreads();
   if (e >= a.n) return;  // wave-uniform; no workgroup barrier below
-  const int G = g.G, R = g.R, WPR = g.WPR, NW = g.NW, D = g.D;
-  float* base = smem + wv * wave_lds_floats(G, R, WPR, NW, D);
+  const float* tdist = smem;
+  const float* tpos = smem + 72;
+  const float* tvis = smem + 328;
+  float* base = smem + wave_hdr_floats(g.C, R) + wv * wave_lds_floats(G, R, WPR, NW, D);
   uint64_t* win = reinterpret_cast<uint64_t*>(base);
   uint32_t* lvis = reinterpret_cast<uint32_t*>(base + 2 * wave_win_words(G, R, WPR));
   float* row = base + 2 * wave_win_words(G, R, WPR) + ((7 * NW + 3) & ~3);
@@ -1459,16 +1475,17 @@ __global__ __launch_bounds__(64 * kWaveEnvs) void pe_step_wave(StepArgs a) {
   // ---- observation (plantos_env.py:251-315) into the LDS row
   const int xp = s.x, yp = s.y;
   for (int i = lane; i < g.C; i += 64) {
-    const signed char* dxr = st.ldx + i * R;
-    const signed char* dyr = st.ldy + i * R;
+    const uint4* orow = reinterpret_cast<const uint4*>(lofs + i * RP);
     int dist = R, ent = EMPTY;
-    for (int r0 = 0; r0 < R; r0 += 8) {  // offsets of 8 probes in flight, then their codes
+    for (int r0 = 0; r0 < R; r0 += 8) {  // 8 probes per 16-B offset read, their codes in flight together
+      const uint4 o = orow[r0 >> 3];
+      const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
       int cx[8], cy[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int r = r0 + j < R ? r0 + j : R - 1;
-        cx[j] = xp + dxr[r];
-        cy[j] = yp + dyr[r];
+        const uint32_t v = ow[j >> 1] >> (16 * (j & 1));
+        cx[j] = xp + (int)(int8_t)(v & 0xFFu);
+        cy[j] = yp + (int)(int8_t)((v >> 8) & 0xFFu);
       }
       bool hit = false;
 #pragma unroll
@@ -1482,7 +1499,7 @@ __global__ __launch_bounds__(64 * kWaveEnvs) void pe_step_wave(StepArgs a) {
       }
       if (hit) break;
     }
-    row[5 * i] = tab->dist[dist];                                // :288
+    row[5 * i] = tdist[dist];                                    // :288
     row[5 * i + 1] = ent == 0 ? 1.0f : 0.0f;
     row[5 * i + 2] = ent == 1 ? 1.0f : 0.0f;
     row[5 * i + 3] = ent == 2 ? 1.0f : 0.0f;
@@ -1492,9 +1509,9 @@ __global__ __launch_bounds__(64 * kWaveEnvs) void pe_step_wave(StepArgs a) {
     const int gx = xp + lane / 5 - 2, gy = yp + lane % 5 - 2;
     const bool in = gx >= 0 && gx < G && gy >= 0 && gy < G;
     const uint32_t v = in ? (lvis[vword(gx, gy)] >> ((4 * (gy + 2)) & 31)) & 15u : 10u;
-    row[5 * g.C + 2 + lane] = tab->vis[v];
+    row[5 * g.C + 2 + lane] = tvis[v];
   } else if (lane < 27) {
-    row[5 * g.C + lane - 25] = tab->pos[lane == 25 ? xp : yp];   // :294-296
+    row[5 * g.C + lane - 25] = tpos[lane == 25 ? xp : yp];       // :294-296
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
@@ -1522,7 +1539,7 @@ __global__ __launch_bounds__(64 * kWaveEnvs) void pe_step_wave(StepArgs a) {
         ns = coop_apply_reset<MAXW>(st, g, e, ns, keep, rw, lane);
       } else {
         ns = coop_reset_env<MAXW>(st, g, rl, e, s.episode, keep, rw, lane, win);
-        coop_fresh_obs<MAXW>(g, rw, ns, row, tab->dist, tab->pos, tab->vis, st.ldx, st.ldy, lane);
+        coop_fresh_obs<MAXW>(g, rw, ns, row, tdist, tpos, tvis, st.ldx, st.ldy, lane);
       }
       if (lane == 0) {
         if (a.pf.scal) a.pf.flag[e] = 1;  // its next map goes into the next generating batch
@@ -2011,7 +2028,8 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
       case V_C64R6: hipLaunchKernelGGL((pe_step_fast<64, 6, false>), grid, block, lds, s, a); break;
       default: {  // pe_step_wave: one wave per env
         const Geo& g = h->g;
-        const size_t wlds = sizeof(float) * kWaveEnvs * (size_t)wave_lds_floats(g.G, g.R, g.WPR, g.NW, g.D);
+        const size_t wlds = sizeof(float) * ((size_t)wave_hdr_floats(g.C, g.R) +
+                                             kWaveEnvs * (size_t)wave_lds_floats(g.G, g.R, g.WPR, g.NW, g.D));
         dim3 wgrid((unsigned)((h->n + kWaveEnvs - 1) / kWaveEnvs)), wblock(64 * kWaveEnvs);
         if (g.WPR == 1)
           hipLaunchKernelGGL(pe_step_wave<1>, wgrid, wblock, wlds, s, a);
