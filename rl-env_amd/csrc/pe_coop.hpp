@@ -612,7 +612,7 @@ __device__ __forceinline__ void coop_load_prefetched(const Prefetch& pf, const G
       if (MAXW == 1 || w < g.WPR) L.rw.set(w, src[w]);
   }
   if constexpr (PfLoad<MAXW, KD>::kEarly) {
-    const float* osrc = pf.obs + e * g.D;
+    const float* osrc = pf_obs_row(pf, e);
 #pragma unroll
     for (int j = 0; j < KD; ++j) L.ov[j] = lane + 64 * j < g.D ? osrc[lane + 64 * j] : 0.0f;
   }
@@ -634,7 +634,7 @@ __device__ __forceinline__ bool coop_take_prefetched(const Prefetch& pf, const G
     for (int j = 0; j < KD; ++j)
       if (lane + 64 * j < g.D) out[lane + 64 * j] = L.ov[j];
   } else {
-    const float* osrc = pf.obs + e * g.D;
+    const float* osrc = pf_obs_row(pf, e);
     for (int k = lane; k < g.D; k += 64) out[k] = osrc[k];
   }
   return true;
@@ -779,8 +779,75 @@ __device__ inline void coop_fresh_obs(const Geo& g, const Row4<MAXW>& rw, const 
 // bytes per env) copied into a byte-coded tile row, once the record is taken.
 __device__ __forceinline__ void coop_copy_record_codes(const Prefetch& pf, const Geo& g, int64_t e, uint8_t* out,
                                                        int lane) {
-  const uint8_t* src = reinterpret_cast<const uint8_t*>(pf.obs) + e * g.D;
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(pf_obs_row(pf, e));
   for (int k = lane; k < g.D; k += 64) out[k] = src[k];
+}
+
+// ---- A block's single done env: its prefetched record staged into LDS by LDS-DMA
+// (global_load_lds_dwordx4: no VGPRs, so it can be issued by the commit wave before
+// the done barrier, at the end of the commit, and land during the barrier and the
+// other waves' last work instead of after it).  16-B units, in lane order:
+//   [0] record scalars  [1, 1+NG) record grid rows  [1+NG, 1+NG+NO) record obs row
+//   [1+NG+NO, 1+2NG+NO) the env's current grid rows (for the terminal info; staged when
+//   all of it fits one instruction, and without the curriculum, whose commit stores rows)
+__host__ __device__ constexpr int pf_grid_units(int G, int WPR) { return (G * WPR + 1) / 2; }
+__host__ __device__ constexpr int pf_stage_units(int G, int WPR, int ostride, bool info) {
+  return 1 + pf_grid_units(G, WPR) * (info ? 2 : 1) + ostride / 16;
+}
+__host__ __device__ constexpr bool pf_stage_info_fits(int G, int WPR, int ostride) {
+  return pf_stage_units(G, WPR, ostride, true) <= 64;
+}
+__host__ __device__ constexpr int pf_stage_bytes(int G, int WPR, int ostride) {
+  return ((pf_stage_units(G, WPR, ostride, pf_stage_info_fits(G, WPR, ostride)) + 63) / 64) * 1024;
+}
+
+// Issue the staging loads of env e's record into lds (wave-uniform; all 64 lanes).
+__device__ __forceinline__ void pf_stage_issue(const Prefetch& pf, const State& st, const Geo& g, int64_t e,
+                                               float* lds, int lane, bool info) {
+  const int ng = pf_grid_units(g.G, g.WPR), no = (int)pf.ostride / 16;
+  const int total = 1 + ng * (info ? 2 : 1) + no;
+  // unit u's address, branch-free (selects on 64-bit integers)
+  const uint64_t rs = reinterpret_cast<uint64_t>(pf.scal + e);
+  const uint64_t rg = reinterpret_cast<uint64_t>(pf.grid + e * g.gstride) - 16u;
+  const uint64_t ro = reinterpret_cast<uint64_t>(pf_obs_row(pf, e)) - 16u * (uint64_t)(1 + ng);
+  const uint64_t cg = reinterpret_cast<uint64_t>(st.grid + e * g.gstride) - 16u * (uint64_t)(1 + ng + no);
+  for (int c = 0; c < total; c += 64) {
+    const int u = c + lane < total ? c + lane : total - 1;
+    const uint64_t b = u == 0 ? rs : (u <= ng ? rg : (u <= ng + no ? ro : cg));
+    const uint64_t ad = b + (u == 0 ? 0u : 16u * (uint64_t)u);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ad),
+                                     (__attribute__((address_space(3))) void*)(lds + 4 * c), 16, 0, 0);
+  }
+}
+
+// Lane r's grid row r from staged rows (words [G][WPR]).
+template <int MAXW>
+__device__ __forceinline__ Row4<MAXW> pf_stage_rows(const uint64_t* w, const Geo& g, int lane) {
+  Row4<MAXW> r{0ull, 0ull, 0ull, 0ull};
+  if (lane < g.G) {
+#pragma unroll
+    for (int k = 0; k < MAXW; ++k)
+      if (MAXW == 1 || k < g.WPR) r.set(k, w[lane * g.WPR + k]);
+  }
+  return r;
+}
+
+// coop_take_prefetched from the staged record (after the wave's vmcnt(0)).
+template <int MAXW, typename OT>
+__device__ __forceinline__ bool pf_stage_take(const float* lds, const Geo& g, int ostride, uint32_t episode,
+                                              Row4<MAXW>& rw, Scal& s, OT* out, int lane) {
+  const uint4 ps = *reinterpret_cast<const uint4*>(lds);
+  const uint32_t key = (uint32_t)__builtin_amdgcn_readfirstlane((int)ps.w);
+  if (key != episode + 1u) return false;
+  s = unpack(make_uint4((uint32_t)__builtin_amdgcn_readfirstlane((int)ps.x),
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)ps.y),
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)ps.z), key));
+  const int ng = pf_grid_units(g.G, g.WPR);
+  rw = pf_stage_rows<MAXW>(reinterpret_cast<const uint64_t*>(lds + 4), g, lane);
+  const OT* o = reinterpret_cast<const OT*>(lds + 4 + 4 * ng);
+  for (int k = lane; k < g.D; k += 64) out[k] = o[k];
+  (void)ostride;
+  return true;
 }
 
 }  // namespace pe

@@ -97,12 +97,19 @@ struct State {
 struct Prefetch {
   uint4* scal;      // [N] packed scalars the reset produces (before coop_apply_reset)
   uint64_t* grid;   // [N][gstride] grid rows of the new map
-  float* obs;       // [N][D] fresh observation of the new episode
+  float* obs;       // [N] rows of ostride bytes: the fresh observation of the new episode (D floats,
+                    // or D byte codes for a byte-coded tile), rows 16-B aligned (LDS-DMA staging)
   uint8_t* flag;    // [N] 1: the env consumed its record (a plain byte store by the step
                     // kernel -- no returning atomic on its critical path)
   uint32_t* queue;  // [N] flagged envs, compacted by pe_pf_compact_kernel (the next batch to generate)
   uint32_t* qn;     // [0] queued count, [1] ticket of the generating launch
+  uint32_t ostride; // bytes per obs row (multiple of 16)
 };
+
+// The record's obs row of env e (floats or codes).
+__device__ __forceinline__ float* pf_obs_row(const Prefetch& pf, int64_t e) {
+  return reinterpret_cast<float*>(reinterpret_cast<char*>(pf.obs) + e * (int64_t)pf.ostride);
+}
 
 struct Rules {
   double r_goal, r_mistake, r_invalid, r_water_empty, r_step, r_exploration, r_revisit, r_complete;

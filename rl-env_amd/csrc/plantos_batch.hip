@@ -554,7 +554,8 @@ __device__ __forceinline__ bool quad_coop(const StepArgs& a, int ndone) {
 template <int NW, bool ONEWORD, int KD, bool BT = false>  // one copy per kernel: each inherits its kernel's register budget
 __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, int C, int R, int lane, int wv, int CW,
                                                 int64_t e0, bool done, uint4 sp, double ret, int ndone, bool wfix,
-                                                const float* ctab = nullptr) {
+                                                const float* ctab = nullptr, const float* stage = nullptr,
+                                                bool stage_info = false) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const StepArgs& a = *reinterpret_cast<const StepArgs*>(ka);
   const Geo& g = a.g;
@@ -595,8 +596,9 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
       const int l = __ffsll((unsigned long long)dmw) - 1;
       const int64_t el = e0 + l;
       OT* orow = rows + l * g.D;
+      // the record: staged into LDS before the done barrier (stage), or loaded now
       PfLoad<MAXW, KD> pl;
-      if (a.pf.scal) coop_load_prefetched<MAXW, KD>(a.pf, g, el, pl, lane);  // in flight from here on
+      if (a.pf.scal && !stage) coop_load_prefetched<MAXW, KD>(a.pf, g, el, pl, lane);  // in flight from here on
       bool keep = false;
       if (done && st.cur) keep = curriculum_on_reset(st.cur, e, rl);  // A2C_training.py:56-95
       const bool kp = __builtin_amdgcn_readlane((int)keep, l) != 0;
@@ -611,14 +613,25 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
       }
       // with the curriculum the commit stored this env's rows: they must land before
       // the info reads them and the reset rewrites them
-      if (st.cur) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (st.cur || stage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (stage: the LDS-DMA landed)
       PE_DSTAMP(1);
-      if (a.tinfo) coop_write_info<MAXW>(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, wf);
+      if (a.tinfo) {
+        if (stage_info)  // the env's rows came with the record
+          coop_info_store<MAXW>(st, g,
+                                pf_stage_rows<MAXW>(reinterpret_cast<const uint64_t*>(
+                                                        stage + 4 + 4 * pf_grid_units(g.G, g.WPR) + a.pf.ostride / 4),
+                                                    g, lane),
+                                sv, a.tinfo + el * PE_NINFO, lane, wf, ltab);
+        else
+          coop_write_info<MAXW>(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, wf);
+      }
       PE_DSTAMP(2);
       Row4<MAXW> rw;
       Scal ns;
       asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
-      if (a.pf.scal && take(el, sv.episode, pl, rw, ns, orow)) {
+      const bool took = stage ? pf_stage_take<MAXW>(stage, g, (int)a.pf.ostride, sv.episode, rw, ns, orow, lane)
+                              : (a.pf.scal && take(el, sv.episode, pl, rw, ns, orow));
+      if (took) {
         ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane);
       } else {
         uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
@@ -1055,6 +1068,11 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   }
   const int xp = s.x + dxv, yp = ok ? ny : s.y;
   const uint32_t nib = n < 15u ? n + 1u : 15u;                    // :203
+  float* stage = smem + (BT ? quad_ctab_off<R, C>() + 256 : quad_tile_off<R>() + EPB * (5 * C + 27));
+  // (byte-coded tiles only: 64x64 desynchronized 37.2 -> 36.5 us; at 20x20 the extra
+  // commit-wave work cost more than the round trip it hides: 11.58 -> 11.87 us)
+  const bool stage_ok = BT && a.pf.scal && quad_coop(a, 1) && e0 + EPB <= a.n;  // full block: every lane live
+  const bool stage_info = !st.cur && a.tinfo && pf_stage_info_fits(g.G, g.WPR, (int)a.pf.ostride);
   OT* row = rows + lane * g.D;
   bool done = false, wfix = false;
   if (live) {
@@ -1117,6 +1135,16 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
       // store of this step can land after the reset's (unless the curriculum
       // carries the visits over)
       wfix = watered && done && a.autoreset && !st.cur;
+      // a full block with a single done env: its prefetched record (and, small grids,
+      // its rows for the terminal info) go into LDS by LDS-DMA from here -- before the
+      // commit's stores (the compiler drains every outstanding memory op before an
+      // LDS-DMA) -- landing during the stores, the barrier and the other waves' last
+      // work (pe_coop.hpp pf_stage_issue)
+      if (BT && stage_ok) {
+        const uint64_t dm1 = __ballot(done);
+        if (__popcll(dm1) == 1)
+          pf_stage_issue(a.pf, st, g, e0 + (__ffsll((unsigned long long)dm1) - 1), stage, lane, stage_info);
+      }
       if (!(done && a.autoreset && !st.cur)) {
         if (ok) {
           // the byte holding the target's visit nibble (padded column p), rebuilt from
@@ -1189,8 +1217,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   static_assert(5 * 4 * EPB + 8 <= (NR * 8 + NV * 4) * EPB, "reset staging must fit the window region");
   const int64_t valid = a.n - e0 < EPB ? a.n - e0 : EPB;
   if (__builtin_expect(any_done, 0)) {  // cold: laid out after the hot path
+    const bool staged = stage_ok && ndone == 1;
     const uint4 ns = quad_done_path<NW, ONEWORD, (5 * C + 27 + 63) / 64, BT>(
-        kernargs(), quad_tile_off<R>(), C, R, lane, wv, CW, e0, done, pack(s), ret, ndone, wfix, ctab);
+        kernargs(), quad_tile_off<R>(), C, R, lane, wv, CW, e0, done, pack(s), ret, ndone, wfix, ctab,
+        staged ? stage : nullptr, staged && stage_info);
     s = unpack(ns);
   }
   // the obs tile goes out through the waves other than the commit wave: its state
@@ -1257,7 +1287,7 @@ __host__ __device__ constexpr int wave_hdr_floats(int C, int R) { return 344 + C
 constexpr int kWaveEnvs = 8;  // envs (waves) per workgroup
 
 template <int MAXW>  // the cooperative reset's row words (1 or kCoopWPR)
-__global__ __launch_bounds__(64 * kWaveEnvs) void pe_step_wave(StepArgs a) {
+__global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(8))) void pe_step_wave(StepArgs a) {  // <= 64 VGPRs
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const Geo& g = a.g;
   const Rules& rl = a.rl;
@@ -1644,10 +1674,10 @@ __global__ __launch_bounds__(256) void pe_prefetch_kernel(StepArgs a, int all) {
         if (MAXW == 1 || w < g.WPR) dst[w] = rw.get(w);
     }
     if constexpr (BT)
-      coop_fresh_obs<MAXW>(g, rw, s, reinterpret_cast<uint8_t*>(pf.obs) + e * g.D, smem, smem + 72, smem + 328,
+      coop_fresh_obs<MAXW>(g, rw, s, reinterpret_cast<uint8_t*>(pf_obs_row(pf, e)), smem, smem + 72, smem + 328,
                            a.st.ldx, a.st.ldy, lane);
     else
-      coop_fresh_obs<MAXW>(g, rw, s, pf.obs + e * g.D, smem, smem + 72, smem + 328, a.st.ldx, a.st.ldy, lane);
+      coop_fresh_obs<MAXW>(g, rw, s, pf_obs_row(pf, e), smem, smem + 72, smem + 328, a.st.ldx, a.st.ldy, lane);
     if (lane == 0) pf.scal[e] = pack(s);  // read by a later launch only
   }
   if (!all) {
@@ -1985,11 +2015,16 @@ enum Variant {
   V_QUAD_C16R4_1W = 9, V_QUAD_C16R4 = 10  // test_environment.py:24 (G=15, C=16, R=4)
 };
 
+// the prefetched records' obs row stride (bytes; pe_device.hpp Prefetch)
+size_t pf_ostride(const Geo& g, bool codes) { return align_up((size_t)(codes ? g.D : 4 * g.D), 16); }
+
 size_t quad_lds_bytes(const Geo& g, bool codes) {
   const size_t off = (size_t)((kTabFloats + (2 * g.R + 3) * kQuadEnvs * 2 + 7 * kQuadEnvs + 3) & ~3);
+  // + the single-done record's LDS-DMA staging region (pe_coop.hpp pf_stage_issue)
+  const size_t stage = (size_t)pf_stage_bytes(g.G, g.WPR, (int)pf_ostride(g, codes));
   if (codes)  // byte tile + code table (quad_ctab_off)
-    return sizeof(float) * (off + (size_t)((kQuadEnvs * g.D + 15) / 16) * 4 + 256);
-  return sizeof(float) * (off + (size_t)kQuadEnvs * g.D);
+    return sizeof(float) * (off + (size_t)((kQuadEnvs * g.D + 15) / 16) * 4 + 256) + stage;
+  return sizeof(float) * (off + (size_t)kQuadEnvs * g.D) + stage;
 }
 
 bool is_quad(int v) { return v >= V_QUAD_C16R6_1W; }
@@ -2374,7 +2409,8 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
       return o;
     };
     const size_t p_scal = pcarve(n * sizeof(uint4)), p_grid = pcarve(n * (size_t)g.gstride * 8);
-    const size_t p_obs = pcarve(n * (size_t)g.D * 4), p_q = pcarve(n * 4), p_qn = pcarve(2 * 4);
+    const uint32_t ostride = (uint32_t)pf_ostride(g, h->tile_codes);
+    const size_t p_obs = pcarve(n * (size_t)ostride), p_q = pcarve(n * 4), p_qn = pcarve(2 * 4);
     const size_t p_flag = pcarve(n);
     if (hipMalloc(&h->pf_mem, po) != hipSuccess || hipMemset(h->pf_mem, 0, po) != hipSuccess) {
       if (h->pf_mem) (void)hipFree(h->pf_mem);
@@ -2388,6 +2424,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
     h->pf.scal = reinterpret_cast<uint4*>(pb + p_scal);
     h->pf.grid = reinterpret_cast<uint64_t*>(pb + p_grid);
     h->pf.obs = reinterpret_cast<float*>(pb + p_obs);
+    h->pf.ostride = ostride;
     h->pf.queue = reinterpret_cast<uint32_t*>(pb + p_q);
     h->pf.qn = reinterpret_cast<uint32_t*>(pb + p_qn);
     h->pf.flag = reinterpret_cast<uint8_t*>(pb + p_flag);
