@@ -471,6 +471,12 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
 // store, 2 = no ray-march, 4 = no round-2 window loads, 8 = no state commit,
 // 16 = no visit-row loads, 32 = no grid-row loads, 64 = timing probe: the block's
 // whole grid + visit blocks streamed in round 1 (coalesced) instead of round 2.
+#ifndef PE_GRID_R1
+#define PE_GRID_R1 1  // one-word sector kernel: the grid block in round 1 (A/B: -DPE_GRID_R1=0)
+#endif
+#ifndef PE_VIS_R1
+#define PE_VIS_R1 0  // ... and the visit block too: no second round (A/B: -DPE_VIS_R1=1)
+#endif
 #ifdef PE_ABLATE
 constexpr int kAblate = PE_ABLATE;
 #else
@@ -851,6 +857,32 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   const int32_t alo = ap[ec << ash], ahi = ap[(ec << ash) + ash];
   double ret = st.ep_ret[wv == CW ? ec : 0];  // (the commit wave's; the others read one shared word)
   const uint4 lw = st.scal[elc];
+  // one-word rows (G <= 20): the loader env's whole grid block (gstride / 2 <= 10
+  // 16-B units, contiguous, 3 per loader thread) comes in round 1 -- its address does
+  // not depend on the position -- and only the visit rows are left for round 2
+  constexpr int JG1 = 3;
+  constexpr bool kGridR1 = ONEWORD && PE_GRID_R1;
+  uint4 qg1[kGridR1 ? JG1 : 1];
+  if constexpr (kGridR1) {
+    const uint4* lgq = reinterpret_cast<const uint4*>(st.grid + elc * g.gstride);
+    const int nq = (int)(g.gstride >> 1);
+#pragma unroll
+    for (int j = 0; j < JG1; ++j) {
+      const int q = sub + LT * j;
+      qg1[j] = lgq[q < nq ? q : nq - 1];
+    }
+  }
+  constexpr int JV1 = 5;  // G <= 20 visit rows of 16 B (NW == 4)
+  constexpr bool kVisR1 = kGridR1 && PE_VIS_R1;
+  uint4 qv1[kVisR1 ? JV1 : 1];
+  if constexpr (kVisR1) {
+    const uint4* lvq = reinterpret_cast<const uint4*>(st.vis + elc * g.vstride);
+#pragma unroll
+    for (int j = 0; j < JV1; ++j) {
+      const int q = sub + LT * j;
+      qv1[j] = lvq[q < g.G ? q : g.G - 1];
+    }
+  }
   if constexpr ((kAblate & 64) != 0) {  // diagnostic only: whole-block streaming probe
     const uint4* gsrc = reinterpret_cast<const uint4*>(st.grid + e0 * g.gstride);
     const uint4* vsrc = reinterpret_cast<const uint4*>(st.vis + e0 * g.vstride);
@@ -910,26 +942,49 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
     if constexpr (ONEWORD) {
       // row pairs (16 B, aligned: env blocks are 16-B aligned, pairs start on even rows)
       const int ps = base & ~1;
-      constexpr int NP = (NR + 2) / 2, JG = (NP + LT - 1) / LT, JV = (NV + LT - 1) / LT;
+      constexpr int NP = (NR + 2) / 2, JG = kGridR1 ? 1 : (NP + LT - 1) / LT, JV = (NV + LT - 1) / LT;
       const int gmax = g.G - 2 > 0 ? g.G - 2 : 0;
       uint4 qg[JG], qv[JV];
+      if constexpr (!kGridR1) {
 #pragma unroll
-      for (int j = 0; j < JG; ++j) {
-        const int ra = ps + 2 * (sub + LT * j);
-        const int rc = ra < 0 ? 0 : (ra > gmax ? gmax : ra);
-        qg[j] = *reinterpret_cast<const uint4*>(lgb + rc);
+        for (int j = 0; j < JG; ++j) {
+          const int ra = ps + 2 * (sub + LT * j);
+          const int rc = ra < 0 ? 0 : (ra > gmax ? gmax : ra);
+          qg[j] = *reinterpret_cast<const uint4*>(lgb + rc);
+        }
       }
       const uint32_t* lvb = st.vis + el * g.vstride;
+      if constexpr (!kVisR1) {
 #pragma unroll
-      for (int j = 0; j < JV; ++j) {
-        const int xr = lx - 3 + sub + LT * j;
-        const int xc = xr < 0 ? 0 : (xr >= g.G ? g.G - 1 : xr);
-        qv[j] = *reinterpret_cast<const uint4*>(lvb + (int64_t)xc * 4);  // g.NW == 4
+        for (int j = 0; j < JV; ++j) {
+          const int xr = lx - 3 + sub + LT * j;
+          const int xc = xr < 0 ? 0 : (xr >= g.G ? g.G - 1 : xr);
+          qv[j] = *reinterpret_cast<const uint4*>(lvb + (int64_t)xc * 4);  // g.NW == 4
+        }
+      }
+      if constexpr (kGridR1) {
+        // the block's rows (pairs 2q, 2q+1) inside the window, then the off-map rows
+        const int nq = (int)(g.gstride >> 1);
+#pragma unroll
+        for (int j = 0; j < JG1; ++j) {
+          const int q = sub + LT * j, ka = 2 * q - base;
+          if (q < nq) {
+            const uint64_t lo = (uint64_t)qg1[j].x | ((uint64_t)qg1[j].y << 32);
+            const uint64_t hi = (uint64_t)qg1[j].z | ((uint64_t)qg1[j].w << 32);
+            if (ka >= 0 && ka < NR) lrow[ka * EPB + le] = lo;
+            if (ka + 1 >= 0 && ka + 1 < NR && 2 * q + 1 < g.G) lrow[(ka + 1) * EPB + le] = hi;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < (NR + LT - 1) / LT; ++j) {
+          const int k = sub + LT * j, xr = base + k;
+          if (k < NR && (xr < 0 || xr >= g.G)) lrow[k * EPB + le] = kEven64;  // off-map rows: obstacles
+        }
       }
 #pragma unroll
       for (int j = 0; j < JG; ++j) {
         const int pp = sub + LT * j;
-        if (pp < NP && !(kAblate & 32)) {
+        if (!kGridR1 && pp < NP && !(kAblate & 32)) {
           const int ra = ps + 2 * pp;
           const int rc = ra < 0 ? 0 : (ra > gmax ? gmax : ra);
           const uint64_t lo = (uint64_t)qg[j].x | ((uint64_t)qg[j].y << 32);
@@ -945,10 +1000,28 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
       // visit rows: one 16-B row per load, funnel-shifted to ybv
       const int lybv = ly > 0 ? ly - 1 : 0;
       const int vw = (4 * lybv) >> 5, vo = (4 * lybv) & 31;
+      if constexpr (kVisR1) {
+        // the block's rows inside the window, then the off-map rows (visit 10: 1.0)
+#pragma unroll
+        for (int j = 0; j < JV1; ++j) {
+          const int xr = sub + LT * j, k = xr - (lx - 3);
+          if (xr < g.G && k >= 0 && k < NV) {
+            const uint4 q = qv1[j];
+            const uint32_t lo = vw == 0 ? q.x : (vw == 1 ? q.y : q.z);
+            const uint32_t hi = vw == 0 ? q.y : (vw == 1 ? q.z : q.w);
+            lvis[k * EPB + le] = vo ? ((lo >> vo) | (hi << (32 - vo))) : lo;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < JV; ++j) {
+          const int k = sub + LT * j, xr = lx - 3 + k;
+          if (k < NV && (xr < 0 || xr >= g.G)) lvis[k * EPB + le] = 0xAAAAAAAAu;
+        }
+      }
 #pragma unroll
       for (int j = 0; j < JV; ++j) {
         const int k = sub + LT * j;
-        if (k < NV && !(kAblate & 16)) {
+        if (!kVisR1 && k < NV && !(kAblate & 16)) {
           const int xr = lx - 3 + k;
           uint32_t lo = 0xAAAAAAAAu, hi = 0xAAAAAAAAu;  // off-map row: visit 10 (reads 1.0)
           if (xr >= 0 && xr < g.G) {
