@@ -923,6 +923,32 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   }
   const int nx = s.x + dxm, ny = s.y + dym;
   const bool inb = mv && nx >= 0 && nx < g.G && ny >= 0 && ny < g.G;  // :193-195
+  // A block whose only env to truncate this step is known from its step count
+  // (:177, the steady state of desynchronized episodes: ~6 % of the blocks each
+  // step): that env's prefetched record -- and, small grids, its current rows for the
+  // terminal info -- go into LDS by LDS-DMA now, in the same round trip as round 2,
+  // so its auto-reset (quad_done_path) makes no memory round trip of its own
+  // (pe_coop.hpp pf_stage_issue; the LDS-DMA needs no VGPRs).  A termination is not
+  // predictable: a block with one then takes the unstaged path.  Byte-coded kernels
+  // only (64x64 desynchronized: 36.6 -> 36.2 us): at 20x20 the waits hipcc places
+  // around a possibly outstanding LDS-DMA (a vmcnt(0) at the next use of any load
+  // result) serialize round 2 in every block (9.39 -> 10.0 us, desync 11.52 -> 12.29).
+  float* stage = smem + (BT ? quad_ctab_off<R, C>() + 256 : quad_tile_off<R>() + EPB * (5 * C + 27));
+  const bool stage_ok = BT && a.pf.scal && quad_coop(a, 1) && e0 + EPB <= a.n;  // full block: every lane live
+  const bool stage_info = !st.cur && a.tinfo && pf_stage_info_fits(g.G, g.WPR, (int)a.pf.ostride);
+  // (issued right after round 2's own loads: hipcc drains every memory op in flight
+  // before the first use of a load result while an LDS-DMA is outstanding, so issued
+  // earlier it would put a round trip of its own ahead of round 2)
+  int npred = 0;
+  uint64_t pm = 0ull;
+  if (stage_ok) {
+    pm = __ballot(s.step + 1 >= rl.max_steps);
+    npred = __popcll(pm);
+  }
+  auto stage_issue = [&]() {
+    if (BT && wv == CW && npred == 1)
+      pf_stage_issue(a.pf, st, g, e0 + (__ffsll((unsigned long long)pm) - 1), stage, lane, stage_info);
+  };
   const int nyc = inb ? ny : s.y;
   const int yb = ONEWORD ? 0 : (s.y > 0 ? s.y - 1 : 0);
   const int ybv = s.y > 0 ? s.y - 1 : 0;
@@ -962,6 +988,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
           qv[j] = *reinterpret_cast<const uint4*>(lvb + (int64_t)xc * 4);  // g.NW == 4
         }
       }
+      stage_issue();
       if constexpr (kGridR1) {
         // the block's rows (pairs 2q, 2q+1) inside the window, then the off-map rows
         const int nq = (int)(g.gstride >> 1);
@@ -1057,6 +1084,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
         vlo[j] = vb[(int64_t)xc * g.NW];
         vhi[j] = vb[(int64_t)xc * g.NW + 1];  // vw + 1 < NW always (one spare word per row)
       }
+      stage_issue();
 #pragma unroll
       for (int j = 0; j < JG; ++j) {
         const int k = sub + LT * j;
@@ -1141,11 +1169,6 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   }
   const int xp = s.x + dxv, yp = ok ? ny : s.y;
   const uint32_t nib = n < 15u ? n + 1u : 15u;                    // :203
-  float* stage = smem + (BT ? quad_ctab_off<R, C>() + 256 : quad_tile_off<R>() + EPB * (5 * C + 27));
-  // (byte-coded tiles only: 64x64 desynchronized 37.2 -> 36.5 us; at 20x20 the extra
-  // commit-wave work cost more than the round trip it hides: 11.58 -> 11.87 us)
-  const bool stage_ok = BT && a.pf.scal && quad_coop(a, 1) && e0 + EPB <= a.n;  // full block: every lane live
-  const bool stage_info = !st.cur && a.tinfo && pf_stage_info_fits(g.G, g.WPR, (int)a.pf.ostride);
   OT* row = rows + lane * g.D;
   bool done = false, wfix = false;
   if (live) {
@@ -1208,16 +1231,6 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
       // store of this step can land after the reset's (unless the curriculum
       // carries the visits over)
       wfix = watered && done && a.autoreset && !st.cur;
-      // a full block with a single done env: its prefetched record (and, small grids,
-      // its rows for the terminal info) go into LDS by LDS-DMA from here -- before the
-      // commit's stores (the compiler drains every outstanding memory op before an
-      // LDS-DMA) -- landing during the stores, the barrier and the other waves' last
-      // work (pe_coop.hpp pf_stage_issue)
-      if (BT && stage_ok) {
-        const uint64_t dm1 = __ballot(done);
-        if (__popcll(dm1) == 1)
-          pf_stage_issue(a.pf, st, g, e0 + (__ffsll((unsigned long long)dm1) - 1), stage, lane, stage_info);
-      }
       if (!(done && a.autoreset && !st.cur)) {
         if (ok) {
           // the byte holding the target's visit nibble (padded column p), rebuilt from
@@ -1290,7 +1303,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   static_assert(5 * 4 * EPB + 8 <= (NR * 8 + NV * 4) * EPB, "reset staging must fit the window region");
   const int64_t valid = a.n - e0 < EPB ? a.n - e0 : EPB;
   if (__builtin_expect(any_done, 0)) {  // cold: laid out after the hot path
-    const bool staged = stage_ok && ndone == 1;
+    const bool staged = stage_ok && npred == 1 && ndone == 1;  // then the done env is the predicted one
     const uint4 ns = quad_done_path<NW, ONEWORD, (5 * C + 27 + 63) / 64, BT>(
         kernargs(), quad_tile_off<R>(), C, R, lane, wv, CW, e0, done, pack(s), ret, ndone, wfix, ctab,
         staged ? stage : nullptr, staged && stage_info);
