@@ -24,6 +24,7 @@ CFG = {
     "g25": (25, 10, 12, 6, 16),   # the multi-word C16 sector kernel (train_mcts's grid)
     "g15": (15, 6, 8, 4, 16),     # one-word C16R4 sector kernel (test_environment.py:24)
     "g12r2": (12, 4, 6, 2, 10),   # one-word C10R2
+    "g64r32": (64, 100, 120, 32, 64),  # the one-wave-per-env kernel (long rays)
 }
 
 
@@ -49,6 +50,8 @@ def info_rows(b, idx):
     ("g25", 600, 80, 60, None, None, None, None, False),
     ("g15", 600, 80, 60, None, None, None, None, False),
     ("g12r2", 600, 80, 60, None, None, None, None, False),
+    ("g64r32", 192, 50, 40, None, None, None, None, False),
+    ("g64r32", 128, 12, 1, "0", None, None, None, False),    # dense: serial resets (coop_max_done 0)
     ("g21", 256, 12, 1, "0", None, None, None, False),        # the constructor default, dense: lane-per-env path
     ("g20", 256, 12, 1, "64", None, None, None, False),       # every env at once through the cooperative path
     ("g64", 128, 12, 1, "0", None, None, None, False),        # every env at once through the lane-per-env path

@@ -31,7 +31,8 @@ CFG = {
 KERNELS = {
     "g20": "pe_step_quad<C16,R6,1word>", "g25": "pe_step_quad<C16,R6>", "g64": "pe_step_quad<C64,R6>",
     "g21": "pe_step_quad<C10,R2>", "g12r2": "pe_step_quad<C10,R2,1word>", "g15": "pe_step_quad<C16,R4,1word>",
-    "g25r4": "pe_step_quad<C16,R4>",
+    "g25r4": "pe_step_quad<C16,R4>", "g64r32": "pe_step_wave", "g7": "pe_step_wave",
+    "g32": "pe_step_wave",
 }
 
 
@@ -188,7 +189,8 @@ def test_rollout_parity_device_rng(name, n, steps):
     b.close()
 
 
-@pytest.mark.parametrize("name,desync", [("g20", False), ("g20", True), ("g64", False), ("g64", True)])
+@pytest.mark.parametrize("name,desync", [("g20", False), ("g20", True), ("g64", False), ("g64", True),
+                                         ("g64r32", True)])
 def test_full_batch_sampled_parity_and_invariants(name, desync):
     """65536 envs (BASELINE headline 20x20/16 rays and the 64x64/64-ray stress
     config) for 1010+ steps, crossing the 1000-step truncation: the oracle replays
@@ -200,7 +202,7 @@ def test_full_batch_sampled_parity_and_invariants(name, desync):
     cooperative reset paths."""
     cfg = CFG[name]
     G, C, R = cfg[0], cfg[4], cfg[3]
-    n, seed, steps = 65536, 5, 1010 if name == "g64" else 1100
+    n, seed, steps = 65536, 5, 1010 if name.startswith("g64") else 1100
     b = make(cfg, n, seed=seed)
     sample = np.r_[0:64, 30000:30064, 65472:65536]
     ov = OracleVec(cfg, sample, seed)
