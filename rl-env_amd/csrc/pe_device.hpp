@@ -89,6 +89,7 @@ struct State {
   const Tables* tab;
   const signed char* ldx;  // [C][R] LIDAR offsets (generic kernel)
   const signed char* ldy;
+  const int16_t* ldxy;     // [C][(R+7)&~7] (dx & 0xFF) | dy << 8, zero-padded (pe_step_wave's LDS header)
   uint32_t* err_bits;      // OR of error flags raised since the last poll
   CurRec* cur;             // batched CurriculumWrapper records, NULL when disabled
 };

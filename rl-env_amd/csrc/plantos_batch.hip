@@ -1387,9 +1387,10 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
   const float* tsrc = reinterpret_cast<const float*>(tab);
   for (int k = threadIdx.x; k < 344; k += blockDim.x) smem[k] = tsrc[k];
   int16_t* lofs = reinterpret_cast<int16_t*>(smem + 344);
-  for (int k = threadIdx.x; k < g.C * RP; k += blockDim.x) {
-    const int i = k / RP, r = k - i * RP;
-    lofs[k] = r < R ? (int16_t)((uint8_t)st.ldx[i * R + r] | ((int)st.ldy[i * R + r] << 8)) : (int16_t)0;
+  {  // the packed offsets, 16 B per thread and pass (st.ldxy, built by pe_create)
+    const uint4* src = reinterpret_cast<const uint4*>(st.ldxy);
+    uint4* dst = reinterpret_cast<uint4*>(lofs);
+    for (int k = threadIdx.x; k < g.C * RP / 8; k += blockDim.x) dst[k] = src[k];
   }
   __syncthreads();
   if (e >= a.n) return;  // wave-uniform; no workgroup barrier below
@@ -2460,6 +2461,8 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   };
   const size_t o_tab = carve(sizeof(Tables));
   const size_t o_ldx = carve(nl), o_ldy = carve(nl);
+  const int RP = (R + 7) & ~7;
+  const size_t o_ldxy = carve((size_t)C * RP * 2);
   const size_t o_err = carve(sizeof(uint32_t));
   const size_t o_scal = carve(n * sizeof(uint4));
   const size_t o_ret = carve(n * sizeof(double));
@@ -2479,6 +2482,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   h->st.tab = reinterpret_cast<const Tables*>(base + o_tab);
   h->st.ldx = reinterpret_cast<const signed char*>(base + o_ldx);
   h->st.ldy = reinterpret_cast<const signed char*>(base + o_ldy);
+  h->st.ldxy = reinterpret_cast<const int16_t*>(base + o_ldxy);
   h->st.err_bits = reinterpret_cast<uint32_t*>(base + o_err);
   h->st.scal = reinterpret_cast<uint4*>(base + o_scal);
   h->st.ep_ret = reinterpret_cast<double*>(base + o_ret);
@@ -2526,9 +2530,14 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   hipError_t e2 = hipMemcpy(base + o_tab, &tab, sizeof(Tables), hipMemcpyHostToDevice);
   hipError_t e3 = hipMemcpy(base + o_ldx, ldx, nl, hipMemcpyHostToDevice);
   hipError_t e4 = hipMemcpy(base + o_ldy, ldy, nl, hipMemcpyHostToDevice);
+  std::vector<int16_t> ldxy((size_t)C * RP, 0);
+  for (int i = 0; i < C; ++i)
+    for (int r = 0; r < R; ++r)
+      ldxy[(size_t)i * RP + r] = (int16_t)((uint8_t)ldx[i * R + r] | ((int)ldy[i * R + r] << 8));
+  hipError_t e5 = hipMemcpy(base + o_ldxy, ldxy.data(), ldxy.size() * 2, hipMemcpyHostToDevice);
   delete[] ldx;
   delete[] ldy;
-  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess) {
+  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess || e5 != hipSuccess) {
     if (h->pf_mem) (void)hipFree(h->pf_mem);
     (void)hipFree(h->mem);
     delete h;
