@@ -477,6 +477,19 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
 #ifndef PE_VIS_R1
 #define PE_VIS_R1 0  // ... and the visit block too: no second round (A/B: -DPE_VIS_R1=1)
 #endif
+#ifndef PE_STAGGER_GROUPS
+#define PE_STAGGER_GROUPS 4  // sector kernel: the grid's start-delay groups (A/B: -DPE_STAGGER_GROUPS=n)
+#endif
+#ifndef PE_PROBE_NOVIS
+#define PE_PROBE_NOVIS 0  // timing probe only: constant visit window, no visit-row loads
+#endif
+#ifndef PE_PROBE_GRID_CHUNKS
+#define PE_PROBE_GRID_CHUNKS 0  // timing probe only: cap the round-1 grid chunks (16 B) per env
+#endif
+#ifndef PE_PROBE_VIS_LO
+#define PE_PROBE_VIS_LO 0  // timing probe only: load visit window rows PE_PROBE_VIS_LO..PE_PROBE_VIS_HI only
+#define PE_PROBE_VIS_HI 6
+#endif
 #ifdef PE_ABLATE
 constexpr int kAblate = PE_ABLATE;
 #else
@@ -839,7 +852,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   // instruction reads LT consecutive rows of 64/LT envs instead of one row of 64.
   PE_STAMP(0);
   if (a.stagger) {  // de-phase the resident workgroups of a CU (speed only)
-    const int q = (int)(blockIdx.x * 4 / gridDim.x);
+    const int q = (int)(blockIdx.x * PE_STAGGER_GROUPS / gridDim.x);
     for (int i = 0; i < q * a.stagger; ++i) __builtin_amdgcn_s_sleep(8);
   }
   constexpr int LT = NW;
@@ -865,12 +878,21 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   uint4 qg1[kGridR1 ? JG1 : 1];
   if constexpr (kGridR1) {
     const uint4* lgq = reinterpret_cast<const uint4*>(st.grid + elc * g.gstride);
-    const int nq = (int)(g.gstride >> 1);
+    const int nq = PE_PROBE_GRID_CHUNKS > 0 ? PE_PROBE_GRID_CHUNKS : (int)(g.gstride >> 1);
 #pragma unroll
     for (int j = 0; j < JG1; ++j) {
       const int q = sub + LT * j;
       qg1[j] = lgq[q < nq ? q : nq - 1];
     }
+  }
+  // timing probe only (PE_PROBE_NOVIS >= 2): PE_PROBE_NOVIS - 1 extra 16-B chunks per
+  // loader thread in round 1 (the cost of a position-independent visit-window cache)
+  constexpr int JX = PE_PROBE_NOVIS >= 2 ? PE_PROBE_NOVIS - 1 : 1;
+  uint4 qx[JX];
+  if constexpr (PE_PROBE_NOVIS >= 2) {
+    const uint4* lxq = reinterpret_cast<const uint4*>(st.vis + elc * g.vstride);
+#pragma unroll
+    for (int j = 0; j < JX; ++j) qx[j] = lxq[sub + LT * j];
   }
   constexpr int JV1 = 5;  // G <= 20 visit rows of 16 B (NW == 4)
   constexpr bool kVisR1 = kGridR1 && PE_VIS_R1;
@@ -980,10 +1002,12 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
         }
       }
       const uint32_t* lvb = st.vis + el * g.vstride;
-      if constexpr (!kVisR1) {
+      if constexpr (!kVisR1 && !PE_PROBE_NOVIS) {
 #pragma unroll
         for (int j = 0; j < JV; ++j) {
-          const int xr = lx - 3 + sub + LT * j;
+          int kk = sub + LT * j;
+          if (PE_PROBE_VIS_LO > 0 || PE_PROBE_VIS_HI < 6) kk = kk < PE_PROBE_VIS_LO ? PE_PROBE_VIS_LO : (kk > PE_PROBE_VIS_HI ? PE_PROBE_VIS_HI : kk);
+          const int xr = lx - 3 + kk;
           const int xc = xr < 0 ? 0 : (xr >= g.G ? g.G - 1 : xr);
           qv[j] = *reinterpret_cast<const uint4*>(lvb + (int64_t)xc * 4);  // g.NW == 4
         }
@@ -1048,7 +1072,15 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
 #pragma unroll
       for (int j = 0; j < JV; ++j) {
         const int k = sub + LT * j;
-        if (!kVisR1 && k < NV && !(kAblate & 16)) {
+        if (PE_PROBE_NOVIS && k < NV) {  // timing probe: no visit round
+          uint32_t acc = 0u;
+          if constexpr (PE_PROBE_NOVIS >= 2) {
+#pragma unroll
+            for (int i = 0; i < JX; ++i) acc ^= qx[i].x ^ qx[i].y ^ qx[i].z ^ qx[i].w;
+          }
+          lvis[k * EPB + le] = acc == 0x9E3779B9u ? 0x22222222u : 0x11111111u;
+        }
+        if (!kVisR1 && !PE_PROBE_NOVIS && k < NV && !(kAblate & 16)) {
           const int xr = lx - 3 + k;
           uint32_t lo = 0xAAAAAAAAu, hi = 0xAAAAAAAAu;  // off-map row: visit 10 (reads 1.0)
           if (xr >= 0 && xr < g.G) {
