@@ -93,6 +93,13 @@ __device__ __forceinline__ void quad_rays(const uint64_t* lrow, int lane, int kc
   constexpr uint32_t kNZ = 0x55555555u & ((1u << (2 * R)) - 1u);
   const float4* tone = reinterpret_cast<const float4*>(tdist + kOneHotF);
   using T = LidarTab<C, R>;
+  // f32 rows: every table read of the sector first, then the row writes -- in program
+  // order a table read after a row write cannot be hoisted above it (the compiler
+  // cannot tell the tile from the tables), which made each ray wait out two LDS
+  // round trips (read -> lgkmcnt(0) -> write) in turn
+  constexpr bool kF32 = std::is_same<OT, float>::value;
+  float dv[kF32 ? I1 - I0 : 1];
+  float4 ov[kF32 ? I1 - I0 : 1];
 #pragma unroll
   for (int i = I0; i < I1; ++i) {
     uint32_t pk = 0u;
@@ -104,13 +111,9 @@ __device__ __forceinline__ void quad_rays(const uint64_t* lrow, int lane, int kc
     const uint32_t nz = ((pk | (pk >> 1)) & kNZ) | (1u << (2 * R));
     const int f = __builtin_ctz(nz);         // 2(r-1) of the first hit, 2R if none
     const int ent = (int)((pk >> f) & 3u);   // its code (EMPTY if none)
-    if constexpr (std::is_same<OT, float>::value) {
-      row[5 * i] = tdist[(f >> 1) + 1];      // float(r / R), plantos_env.py:288 (R/R if none)
-      const float4 oh = tone[ent];
-      row[5 * i + 1] = oh.x;
-      row[5 * i + 2] = oh.y;
-      row[5 * i + 3] = oh.z;
-      row[5 * i + 4] = oh.w;
+    if constexpr (kF32) {
+      dv[i - I0] = tdist[(f >> 1) + 1];      // float(r / R), plantos_env.py:288 (R/R if none)
+      ov[i - I0] = tone[ent];
     } else {
       row[5 * i] = (uint8_t)((f >> 1) + 1);  // code r = dist[r] (R+1: 1.0, nothing hit)
       const uint32_t oh = (uint32_t)(R + 1) << (8 * ent);  // one-hot as codes {0, R+1}
@@ -118,6 +121,16 @@ __device__ __forceinline__ void quad_rays(const uint64_t* lrow, int lane, int kc
       row[5 * i + 2] = (uint8_t)(oh >> 8);
       row[5 * i + 3] = (uint8_t)(oh >> 16);
       row[5 * i + 4] = (uint8_t)(oh >> 24);
+    }
+  }
+  if constexpr (kF32) {
+#pragma unroll
+    for (int i = I0; i < I1; ++i) {
+      row[5 * i] = dv[i - I0];
+      row[5 * i + 1] = ov[i - I0].x;
+      row[5 * i + 2] = ov[i - I0].y;
+      row[5 * i + 3] = ov[i - I0].z;
+      row[5 * i + 4] = ov[i - I0].w;
     }
   }
 }
@@ -141,12 +154,15 @@ __device__ __forceinline__ void quad_slice_row(const uint32_t* lvis, int lane, i
                                                uint32_t nib, int C, T* row, const float* tvis) {
   uint32_t v = lvis[(dxv + 1 + lx) * kQuadEnvs + lane] >> vs;
   if (lx == 2 && bump) v = (v & ~0xF00u) | (nib << 8);  // the move's own visit (:203)
+  if constexpr (std::is_same<T, float>::value) {
+    float t[5];  // table reads first, then the writes (see quad_rays)
 #pragma unroll
-  for (int ly = 0; ly < 5; ++ly) {
-    if constexpr (std::is_same<T, float>::value)
-      row[5 * C + 2 + 5 * lx + ly] = tvis[(v >> (4 * ly)) & 15u];
-    else
-      row[5 * C + 2 + 5 * lx + ly] = (uint8_t)(kCodeVis + ((v >> (4 * ly)) & 15u));
+    for (int ly = 0; ly < 5; ++ly) t[ly] = tvis[(v >> (4 * ly)) & 15u];
+#pragma unroll
+    for (int ly = 0; ly < 5; ++ly) row[5 * C + 2 + 5 * lx + ly] = t[ly];
+  } else {
+#pragma unroll
+    for (int ly = 0; ly < 5; ++ly) row[5 * C + 2 + 5 * lx + ly] = (uint8_t)(kCodeVis + ((v >> (4 * ly)) & 15u));
   }
 }
 
