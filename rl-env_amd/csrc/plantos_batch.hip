@@ -1537,6 +1537,7 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
     return (int)((win[xr * WPR + (bit >> 6) - w0] >> (bit & 63)) & 3u);
   };
   auto vword = [&](int xr, int col) -> int { return (xr - vlo) * NW + ((4 * (col + 2)) >> 5); };
+  const uint32_t* win32 = reinterpret_cast<const uint32_t*>(win);
 
   // ---- transition (plantos_env.py:160-222), wave-uniform
   s.step = s.step < 65535 ? s.step + 1 : 65535;                 // :162
@@ -1658,24 +1659,28 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
     for (int r0 = 0; r0 < R; r0 += 8) {  // 8 probes per 16-B offset read, their codes in flight together
       const uint4 o = orow[r0 >> 3];
       const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
-      int cx[8], cy[8];
+      // the 8 probe codes packed 2 bits each (probe j at bits 2j), first hit by one
+      // find-first-set (as the sector kernel's quad_rays); 32-bit window reads (a
+      // 2-bit code never straddles a word: its bit offset is even)
+      uint32_t pk = 0u;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const uint32_t v = ow[j >> 1] >> (16 * (j & 1));
-        cx[j] = xp + (int)(int8_t)(v & 0xFFu);
-        cy[j] = yp + (int)(int8_t)((v >> 8) & 0xFFu);
+        const int cx = xp + (int)(int8_t)(v & 0xFFu);
+        const int bit = 2 * (yp + (int)(int8_t)((v >> 8) & 0xFFu) + R);
+        const uint32_t c = (uint32_t)cx < (uint32_t)G  // :271-284 (off-map rows: obstacle)
+                               ? (win32[2 * (cx * WPR - w0) + (bit >> 5)] >> (bit & 31)) & 3u
+                               : (uint32_t)OBST;
+        pk |= c << (2 * j);
       }
-      bool hit = false;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int code = code_at(cx[j], cy[j] + R);  // :271-284 (off-map rows: obstacle)
-        if (!hit && r0 + j < R && code != EMPTY) {
-          hit = true;
-          dist = r0 + j + 1;
-          ent = code;
-        }
+      if (R - r0 < 8) pk &= (1u << (2 * (R - r0))) - 1u;  // the zero-padded offsets past R
+      const uint32_t nz = (pk | (pk >> 1)) & 0x5555u;
+      if (nz) {
+        const int f = __builtin_ctz(nz);  // 2j of the first hit
+        dist = r0 + (f >> 1) + 1;
+        ent = (int)((pk >> f) & 3u);
+        break;
       }
-      if (hit) break;
     }
     row[5 * i] = tdist[dist];                                    // :288
     row[5 * i + 1] = ent == 0 ? 1.0f : 0.0f;
