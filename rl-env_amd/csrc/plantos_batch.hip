@@ -1661,7 +1661,8 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
       const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
       // the 8 probe codes packed 2 bits each (probe j at bits 2j), first hit by one
       // find-first-set (as the sector kernel's quad_rays); 32-bit window reads (a
-      // 2-bit code never straddles a word: its bit offset is even)
+      // 2-bit code never straddles a word: its bit offset is even; the row offset as a
+      // full-rate 24-bit multiply, not the quarter-rate 32-bit one)
       uint32_t pk = 0u;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -1669,7 +1670,7 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
         const int cx = xp + (int)(int8_t)(v & 0xFFu);
         const int bit = 2 * (yp + (int)(int8_t)((v >> 8) & 0xFFu) + R);
         const uint32_t c = (uint32_t)cx < (uint32_t)G  // :271-284 (off-map rows: obstacle)
-                               ? (win32[2 * (cx * WPR - w0) + (bit >> 5)] >> (bit & 31)) & 3u
+                               ? (win32[2 * ((int)__umul24((uint32_t)cx, (uint32_t)WPR) - w0) + (bit >> 5)] >> (bit & 31)) & 3u
                                : (uint32_t)OBST;
         pk |= c << (2 * j);
       }
