@@ -926,7 +926,7 @@ constexpr size_t kMctsLdsMax = 64 * 1024;  // >= 2 workgroups per CU
 
 struct pe_mcts {
   pe_handle* h;
-  int force_global;  // PE_MCTS_GLOBAL=1: the global-memory sim cells even when LDS fits
+  int force_global;  // PE_MCTS_GLOBAL=1 (PE_DEBUG_KNOBS builds): the global-memory sim cells even when LDS fits
   int n_sims, max_depth;
   double c;
   void* mem;
@@ -976,7 +976,10 @@ int pe_mcts_create(pe_handle* h, int32_t n_simulations, double c_param, int32_t 
   m->csg = reinterpret_cast<uint32_t*>(q + al(n * ggp) + al(n * GG * 4));
   m->ggp = (int)ggp;
   m->h = h;
+  m->force_global = 0;
+#ifdef PE_DEBUG_KNOBS  // A/B builds only (tools/ab_build.sh): the product library reads no environment variable
   m->force_global = getenv("PE_MCTS_GLOBAL") && atoi(getenv("PE_MCTS_GLOBAL")) != 0;
+#endif
   m->n_sims = n_simulations;
   m->max_depth = max_depth;
   m->c = c_param;
