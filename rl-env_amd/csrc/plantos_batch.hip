@@ -1432,9 +1432,33 @@ __host__ __device__ constexpr int wave_lds_floats(int G, int R, int WPR, int NW,
 // rounded up to 8 (one 16-B LDS read per 8 probes of a ray).
 __host__ __device__ constexpr int wave_hdr_floats(int C, int R) { return 344 + C * ((R + 7) & ~7) / 2; }
 constexpr int kWaveEnvs = 8;  // envs (waves) per workgroup
+// Rover-aligned window (ALN): after the transition the post-move rows xp-R .. xp+R
+// are re-staged over the raw window, each shifted so that cell yp+dy+R of the
+// padded row sits at bit 2(dy+R) of NWA = ceil((4R+2)/32) words, rows off the map
+// filled with OBST.  A probe (dx, dy) is then word (dx+R)*NWA + (2(dy+R))>>5,
+// shift (2(dy+R))&31 -- constants per (ray, probe) held in the LDS offset table
+// (11-bit word | 5-bit shift << 11), no bounds check and no position arithmetic per
+// probe.  Used when the aligned rows fit the raw region and kAlnSlots words per lane.
+constexpr int kAlnSlots = 8;
+__host__ __device__ constexpr int wave_aln_words(int R) { return (2 * R + 1) * ((4 * R + 33) >> 5); }
+__host__ __device__ constexpr bool wave_aln_ok(int G, int R, int WPR) {
+  return wave_aln_words(R) <= 64 * kAlnSlots && wave_aln_words(R) <= 2 * wave_win_words(G, R, WPR);
+}
+// one packed (dx & 0xFF | dy << 8) offset -> the aligned window's (word | shift << 11)
+__device__ __forceinline__ uint32_t aln_entry(uint32_t v, int R, int NWA) {
+  const int dx = (int)(int8_t)(v & 0xFFu), dy = (int)(int8_t)((v >> 8) & 0xFFu);
+  const int cb = 2 * (dy + R);
+  return (uint32_t)((dx + R) * NWA + (cb >> 5)) | ((uint32_t)(cb & 31) << 11);
+}
+__device__ __forceinline__ uint32_t aln_pair(uint32_t w, int R, int NWA) {
+  return aln_entry(w & 0xFFFFu, R, NWA) | (aln_entry(w >> 16, R, NWA) << 16);
+}
 
-template <int MAXW>  // the cooperative reset's row words (1 or kCoopWPR)
-__global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(8))) void pe_step_wave(StepArgs a) {  // <= 64 VGPRs
+template <int MAXW, bool ALN>  // the cooperative reset's row words (1 or kCoopWPR); rover-aligned rays
+#ifndef PE_WAVE_WPE4  // waves per SIMD of the multi-word variant (A/B builds only): 8 spills
+#define PE_WAVE_WPE4 8  // ~130 B/lane yet beats 7 / 6 (64x64/R=32: 110.1 / 117.3 / 112.8 us)
+#endif
+__global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(MAXW == 1 ? 8 : PE_WAVE_WPE4))) void pe_step_wave(StepArgs a) {  // <= 64 VGPRs at 8
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const Geo& g = a.g;
   const Rules& rl = a.rl;
@@ -1451,7 +1475,14 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
   {  // the packed offsets, 16 B per thread and pass (st.ldxy, built by pe_create)
     const uint4* src = reinterpret_cast<const uint4*>(st.ldxy);
     uint4* dst = reinterpret_cast<uint4*>(lofs);
-    for (int k = threadIdx.x; k < g.C * RP / 8; k += blockDim.x) dst[k] = src[k];
+    for (int k = threadIdx.x; k < g.C * RP / 8; k += blockDim.x) {
+      uint4 v = src[k];
+      if constexpr (ALN) {
+        const int NWA = (4 * R + 33) >> 5;
+        v = make_uint4(aln_pair(v.x, R, NWA), aln_pair(v.y, R, NWA), aln_pair(v.z, R, NWA), aln_pair(v.w, R, NWA));
+      }
+      dst[k] = v;
+    }
   }
   __syncthreads();
   if (e >= a.n) return;  // wave-uniform; no workgroup barrier below
@@ -1653,6 +1684,31 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
 
   // ---- observation (plantos_env.py:251-315) into the LDS row
   const int xp = s.x, yp = s.y;
+  if constexpr (ALN) {  // the rover-aligned window over the raw one (every read before any write)
+    const int NWA = (4 * R + 33) >> 5, tot = (2 * R + 1) * NWA;
+    const uint32_t mg = 0xFFFFFFFFu / (uint32_t)NWA + 1u;  // k / NWA as a high multiply (k < 512; NWA >= 2)
+    const int sw = (2 * yp) >> 5, sb = (2 * yp) & 31;
+    uint32_t av[kAlnSlots];
+#pragma unroll
+    for (int t = 0; t < kAlnSlots; ++t) {
+      const int k = lane + 64 * t;
+      const int i = NWA == 1 ? k : (int)__umulhi((uint32_t)k, mg), w = k - i * NWA;
+      const int xr = xp - R + i;
+      av[t] = 0x55555555u;  // OBST (1) in every cell: rows off the map (:271-284)
+      if (k < tot && (uint32_t)xr < (uint32_t)G) {
+        const int q = 2 * ((int)__umul24((uint32_t)xr, (uint32_t)WPR) - w0) + sw + w;
+        av[t] = __builtin_amdgcn_alignbit(win32[q + 1], win32[q], (uint32_t)sb);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    uint32_t* awin = reinterpret_cast<uint32_t*>(win);
+#pragma unroll
+    for (int t = 0; t < kAlnSlots; ++t) {
+      const int k = lane + 64 * t;
+      if (k < tot) awin[k] = av[t];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
   for (int i = lane; i < g.C; i += 64) {
     const uint4* orow = reinterpret_cast<const uint4*>(lofs + i * RP);
     int dist = R, ent = EMPTY;
@@ -1667,11 +1723,16 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const uint32_t v = ow[j >> 1] >> (16 * (j & 1));
-        const int cx = xp + (int)(int8_t)(v & 0xFFu);
-        const int bit = 2 * (yp + (int)(int8_t)((v >> 8) & 0xFFu) + R);
-        const uint32_t c = (uint32_t)cx < (uint32_t)G  // :271-284 (off-map rows: obstacle)
-                               ? (win32[2 * ((int)__umul24((uint32_t)cx, (uint32_t)WPR) - w0) + (bit >> 5)] >> (bit & 31)) & 3u
-                               : (uint32_t)OBST;
+        uint32_t c;
+        if constexpr (ALN) {  // table word and shift; off-map rows hold OBST
+          c = (win32[v & 0x7FFu] >> ((v >> 11) & 31u)) & 3u;
+        } else {
+          const int cx = xp + (int)(int8_t)(v & 0xFFu);
+          const int bit = 2 * (yp + (int)(int8_t)((v >> 8) & 0xFFu) + R);
+          c = (uint32_t)cx < (uint32_t)G  // :271-284 (off-map rows: obstacle)
+                  ? (win32[2 * ((int)__umul24((uint32_t)cx, (uint32_t)WPR) - w0) + (bit >> 5)] >> (bit & 31)) & 3u
+                  : (uint32_t)OBST;
+        }
         pk |= c << (2 * j);
       }
       if (R - r0 < 8) pk &= (1u << (2 * (R - r0))) - 1u;  // the zero-padded offsets past R
@@ -2220,10 +2281,18 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
         const size_t wlds = sizeof(float) * ((size_t)wave_hdr_floats(g.C, g.R) +
                                              kWaveEnvs * (size_t)wave_lds_floats(g.G, g.R, g.WPR, g.NW, g.D));
         dim3 wgrid((unsigned)((h->n + kWaveEnvs - 1) / kWaveEnvs)), wblock(64 * kWaveEnvs);
-        if (g.WPR == 1)
-          hipLaunchKernelGGL(pe_step_wave<1>, wgrid, wblock, wlds, s, a);
-        else
-          hipLaunchKernelGGL(pe_step_wave<kCoopWPR>, wgrid, wblock, wlds, s, a);
+        const bool aln = wave_aln_ok(g.G, g.R, g.WPR);
+        if (g.WPR == 1) {
+          if (aln)
+            hipLaunchKernelGGL((pe_step_wave<1, true>), wgrid, wblock, wlds, s, a);
+          else
+            hipLaunchKernelGGL((pe_step_wave<1, false>), wgrid, wblock, wlds, s, a);
+        } else {
+          if (aln)
+            hipLaunchKernelGGL((pe_step_wave<kCoopWPR, true>), wgrid, wblock, wlds, s, a);
+          else
+            hipLaunchKernelGGL((pe_step_wave<kCoopWPR, false>), wgrid, wblock, wlds, s, a);
+        }
         break;
       }
     }
