@@ -1454,6 +1454,57 @@ __device__ __forceinline__ uint32_t aln_pair(uint32_t w, int R, int NWA) {
   return aln_entry(w & 0xFFFFu, R, NWA) | (aln_entry(w >> 16, R, NWA) << 16);
 }
 
+// The wave kernel's done path (terminal obs / info, auto-reset), called by the
+// wave of a done env with all lanes active.
+template <int MAXW>
+__device__ __attribute__((noinline)) void wave_done(const StepArgs& a, int64_t e, Scal s, int wfix, float* row,
+                                                    uint64_t* win, const float* tdist, const float* tpos,
+                                                    const float* tvis, int lane) {
+  const Geo& g = a.g;
+  const Rules& rl = a.rl;
+  const State& st = a.st;
+  const Tables* tab = st.tab;
+  const int D = g.D;
+  if (a.tobs)
+    for (int k = lane; k < D; k += 64) a.tobs[e * D + k] = row[k];
+  if (!a.autoreset) {
+    if (a.tinfo && lane == 0) write_info(st, g, tab, e, s, a.tinfo + e * PE_NINFO);
+  } else if (a.coop_max_done > 0) {  // coop_reset_ok geometry (pe_create)
+    constexpr int KD = 6;            // D <= 347 (C <= 64): the record's obs row after its check
+    PfLoad<MAXW, KD> pl;
+    if (a.pf.scal) coop_load_prefetched<MAXW, KD>(a.pf, g, e, pl, lane);  // in flight from here on
+    bool keep = false;
+    if (st.cur && lane == 0) keep = curriculum_on_reset(st.cur, e, rl);  // A2C_training.py:56-95
+    keep = __builtin_amdgcn_readfirstlane((int)keep) != 0;
+    // with the curriculum the commit stored this env's rows: they land before the
+    // info reads them and the reset rewrites them
+    if (st.cur) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.tinfo) coop_write_info<MAXW>(st, g, e, s, a.tinfo + e * PE_NINFO, lane, wfix);
+    Row4<MAXW> rw;
+    Scal ns;
+    asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
+    if (a.pf.scal && coop_take_prefetched<MAXW, KD>(a.pf, g, e, s.episode, pl, rw, ns, row, lane)) {
+      ns = coop_apply_reset<MAXW>(st, g, e, ns, keep, rw, lane);
+    } else {
+      ns = coop_reset_env<MAXW>(st, g, rl, e, s.episode, keep, rw, lane, win);
+      coop_fresh_obs<MAXW>(g, rw, ns, row, tdist, tpos, tvis, st.ldx, st.ldy, lane);
+    }
+    if (lane == 0) {
+      if (a.pf.scal) a.pf.flag[e] = 1;  // its next map goes into the next generating batch
+      st_wt(st.ep_ret + e, 0.0);
+      st_wt(st.scal + e, pack(ns));
+    }
+  } else if (lane == 0) {  // serial reset (the geometry has no cooperative one)
+    if (a.tinfo) write_info(st, g, tab, e, s, a.tinfo + e * PE_NINFO, wfix);
+    const Scal ns = reset_env(st, g, rl, tab, e, s.episode);
+    st_wt(st.ep_ret + e, 0.0);
+    st_wt(st.scal + e, pack(ns));
+    build_obs_fresh(a, st.grid + e * g.gstride, ns, row, tab->dist, tab->pos, tab->vis, st.ldx, st.ldy);
+  }
+  // the LDS row / window are flat accesses here: all of them done before the caller's tile store
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
 template <int MAXW, bool ALN>  // the cooperative reset's row words (1 or kCoopWPR); rover-aligned rays
 #ifndef PE_WAVE_WPE4  // waves per SIMD of the multi-word variant (A/B builds only): 8 spills
 #define PE_WAVE_WPE4 8  // ~130 B/lane yet beats 7 / 6 (64x64/R=32: 110.1 / 117.3 / 112.8 us)
@@ -1760,45 +1811,12 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
-  // ---- DummyVecEnv auto-reset (rare) and terminal outputs
-  if (done) {
-    if (a.tobs)
-      for (int k = lane; k < D; k += 64) a.tobs[e * D + k] = row[k];
-    if (!a.autoreset) {
-      if (a.tinfo && lane == 0) write_info(st, g, tab, e, s, a.tinfo + e * PE_NINFO);
-    } else if (a.coop_max_done > 0) {  // coop_reset_ok geometry (pe_create)
-      constexpr int KD = 6;            // D <= 347 (C <= 64): the record's obs row after its check
-      PfLoad<MAXW, KD> pl;
-      if (a.pf.scal) coop_load_prefetched<MAXW, KD>(a.pf, g, e, pl, lane);  // in flight from here on
-      bool keep = false;
-      if (st.cur && lane == 0) keep = curriculum_on_reset(st.cur, e, rl);  // A2C_training.py:56-95
-      keep = __builtin_amdgcn_readfirstlane((int)keep) != 0;
-      // with the curriculum the commit stored this env's rows: they land before the
-      // info reads them and the reset rewrites them
-      if (st.cur) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (a.tinfo) coop_write_info<MAXW>(st, g, e, s, a.tinfo + e * PE_NINFO, lane, wfix);
-      Row4<MAXW> rw;
-      Scal ns;
-      asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
-      if (a.pf.scal && coop_take_prefetched<MAXW, KD>(a.pf, g, e, s.episode, pl, rw, ns, row, lane)) {
-        ns = coop_apply_reset<MAXW>(st, g, e, ns, keep, rw, lane);
-      } else {
-        ns = coop_reset_env<MAXW>(st, g, rl, e, s.episode, keep, rw, lane, win);
-        coop_fresh_obs<MAXW>(g, rw, ns, row, tdist, tpos, tvis, st.ldx, st.ldy, lane);
-      }
-      if (lane == 0) {
-        if (a.pf.scal) a.pf.flag[e] = 1;  // its next map goes into the next generating batch
-        st_wt(st.ep_ret + e, 0.0);
-        st_wt(st.scal + e, pack(ns));
-      }
-    } else if (lane == 0) {  // serial reset (the geometry has no cooperative one)
-      if (a.tinfo) write_info(st, g, tab, e, s, a.tinfo + e * PE_NINFO, wfix);
-      const Scal ns = reset_env(st, g, rl, tab, e, s.episode);
-      st_wt(st.ep_ret + e, 0.0);
-      st_wt(st.scal + e, pack(ns));
-      build_obs_fresh(a, st.grid + e * g.gstride, ns, row, tab->dist, tab->pos, tab->vis, st.ldx, st.ldy);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // ---- DummyVecEnv auto-reset (rare) and terminal outputs: out of line, so that the
+  // reset path's pointers and state do not shape the hot path's register allocation
+  if (done) {  // the kernel's argument read in place (StepArgs is its only argument): taking
+              // &a would copy the whole struct to scratch on every launch
+    const StepArgs* ap = (const StepArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    wave_done<MAXW>(*ap, e, s, wfix, row, win, tdist, tpos, tvis, lane);
   }
   float* dst = a.obs + e * D;
   for (int k = lane; k < D; k += 64) dst[k] = row[k];
