@@ -15,9 +15,11 @@ this process is one rank; run directly, it starts the N ranks itself
 exits with their status -- or exits non-zero at once if fewer than N GPUs are
 visible.  Each rank owns a disjoint shard of E envs (global ids rank*E ...), no
 collective on the data path ("scaling": "weak"); barrier + max-over-ranks
-timing.  --gather adds the host-boundary RCCL gather of each step's packed
-(obs, reward, terminated, truncated) buffer to rank 0, pipelined behind the next
-step (plantos_amd/shard.py step_gather).
+timing.  `value` is that replica throughput.  Every run then also times the
+host-boundary leg of BASELINE config 5 ("with RCCL gather"): each step's packed
+(obs, reward, terminated, truncated) buffer gathered to rank 0 over RCCL,
+pipelined behind the next step (plantos_amd/shard.py step_gather) -- the line's
+"gather" object (with one rank there is nothing to gather and it says so).
 
 After the headline window the same batch is timed again with desynchronized
 episodes (every env at its own step count: ~n/1000 auto-resets in every step, the
@@ -61,11 +63,13 @@ def parse():
     p.add_argument("--range", type=int, default=6)
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--action-steps", type=int, default=64, help="distinct pre-generated action rows")
-    p.add_argument("--gather", action="store_true",
-                   help="RCCL gather of each step's (obs, reward, done) to rank 0, pipelined")
+    p.add_argument("--gather-steps", type=int, default=500,
+                   help="steps of the gather-every-step leg (RCCL gather of each step's outputs to rank 0, "
+                        "pipelined; the line's 'gather' object; 0: skip it)")
     p.add_argument("--graph", type=int, default=64,
-                   help="capture this many consecutive steps in one hipGraph and replay it (0: one host "
-                        "launch per step); every captured step is a full pe_step launch")
+                   help="capture up to this many consecutive steps in one hipGraph and replay it (0: one host "
+                        "launch per step); every captured step is a full pe_step launch; a window of K <= this "
+                        "many steps is ONE K-step graph")
     p.add_argument("--desync", action="store_true",
                    help="time the desynchronized episode mix as the headline window (default: synchronized "
                         "fresh episodes, desync as the secondary 'desync' object)")
@@ -171,9 +175,50 @@ def measured_traffic(cfg, sha):
 
 
 # ---------------------------------------------------------------- timed windows
+def plan_graph(K, graph_max, pf):
+    """Steps per captured graph for a K-step window (0: direct launches).  A window of
+    K <= graph_max steps is one K-step graph replayed once; a longer one replays a
+    graph whose length is a multiple of the prefetch cadence pf (every replay then
+    holds the same share of prefetch launches), the rest as direct launches."""
+    if graph_max <= 1 or K <= 1:
+        return 0
+    if K <= graph_max:
+        return K
+    chunk = graph_max
+    if pf > 0 and chunk % pf:
+        chunk = chunk * pf // math.gcd(chunk, pf)
+    return min(chunk, K)
+
+
+def launch_label(K, chunk):
+    """What the timed loop of timed() executes for K steps and this chunk."""
+    if not chunk:
+        return f"{K} direct host launches (one pe_step per step)"
+    reps, rest = K // chunk, K % chunk
+    lab = f"hipGraph: {reps} replay{'s' if reps != 1 else ''} of {chunk} captured pe_step launches"
+    return lab + (f" + {rest} direct host launches" if rest else "")
+
+
 def timed(torch, dist, device, K, one_step, chunk, graph, finish=None):
     """K steps bracketed by barrier + synchronize; (wall s, kernel ms per step).
-    finish(): work of the K steps still queued elsewhere (pipelined gathers)."""
+    finish(): work of the K steps still queued elsewhere (pipelined gathers).
+    device None: the CPU plumbing of --selftest (no events; kernel ms = wall)."""
+    if device is None:
+        if dist:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for k in range(K):
+            one_step(k)
+        if finish is not None:
+            finish()
+        if dist:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([elapsed], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t[0])
+        return elapsed, elapsed / K * 1e3
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -214,11 +259,61 @@ def desynchronize(torch, b, seed):
     b.set_state(scalars=sc)
 
 
+def gather_leg(torch, dist, device, shard, Kg, gather_step, world):
+    """BASELINE config 5's host-boundary leg: Kg steps, each step's packed outputs
+    gathered to rank 0 (RCCL over xGMI; gloo in --selftest), pipelined behind the
+    next step.  Host launches: an RCCL collective inside a captured graph is not
+    exercised on the one-GPU boxes this code is tested on, and a hang there would
+    cost the whole scaling run."""
+    for t in range(20):
+        gather_step(t)
+    shard.flush()
+    if device is not None:
+        torch.cuda.synchronize()
+    g_el, _ = timed(torch, dist, device, Kg, gather_step, 0, None, shard.flush)
+    n = shard.n
+    per_rank = shard.io_bytes()
+    us = g_el / Kg * 1e6
+    backend = "RCCL (nccl backend)" if device is not None else "gloo (selftest)"
+    return {"value": n * Kg * world / g_el, "unit": "env-steps/s", "steps": Kg, "us_per_step": us,
+            "bytes_per_rank_per_step": per_rank, "bytes_gathered_per_step": per_rank * world,
+            "root_ingress_bytes_per_step": per_rank * (world - 1),
+            "root_ingress_GBps": per_rank * (world - 1) / (us * 1e-6) / 1e9,
+            "launch": f"{Kg} direct host launches, each step's gather issued async (double-buffered)",
+            "collective": (f"torch.distributed.gather over {backend} to rank 0" if world > 1
+                           else "none: one rank, nothing to gather (the step into the slot buffers only)")}
+
+
+class _SelftestBatch:
+    """--selftest stand-in for PlantOSBatch on the CPU: the io-buffer interface only,
+    outputs = the global env id (plumbing of the shard / gather leg; no env work)."""
+
+    def __init__(self, n, env_id_offset=0, seed=0, obs_dim=107):
+        import torch
+        self.torch, self.num_envs, self.obs_dim, self.device = torch, n, obs_dim, torch.device("cpu")
+        self.ids = torch.arange(env_id_offset, env_id_offset + n, dtype=torch.float32)
+
+    def io_bytes(self):
+        return 4 * self.num_envs * self.obs_dim + 6 * self.num_envs
+
+    def new_io(self):
+        return self.torch.zeros(self.io_bytes(), dtype=self.torch.uint8)
+
+    def step(self, actions, io=None):
+        n, D = self.num_envs, self.obs_dim
+        io[:4 * n * D].view(self.torch.float32).view(n, D).copy_(self.ids[:, None])
+
+    def close(self):
+        pass
+
+
 def selftest_rank(args, world, rank):
     """--selftest: the rank plumbing on the CPU (gloo): world size, barrier,
-    max-over-ranks reduction, one line from rank 0.  No GPU work, no value."""
+    max-over-ranks reduction, the gather leg's collective and its object, one line
+    from rank 0.  No GPU work, no value."""
     import torch
     import torch.distributed as dist
+    from plantos_amd.shard import ShardedPlantOS
     if world > 1:
         dist.init_process_group("gloo")
         assert dist.get_world_size() == world
@@ -226,9 +321,19 @@ def selftest_rank(args, world, rank):
     if world > 1:
         dist.barrier()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    n = 64
+    shard = ShardedPlantOS(n, batch_factory=lambda n_, **kw: _SelftestBatch(n_, **kw))
+    acts = torch.zeros(n, dtype=torch.int64)
+    gather = gather_leg(torch, dist if world > 1 else None, None, shard, 10,
+                        lambda k: shard.step_gather(acts), world)
+    ok = True
+    if rank == 0:  # every rank's slot arrived, in global env order
+        obs = shard.unpack(shard.gathered(0))[0]
+        ok = bool((obs[:, 0] == torch.arange(world * n, dtype=torch.float32)).all())
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "env-steps/s", "n_gpus": world,
-                          "selftest": True, "max_over_ranks": float(t[0])}), flush=True)
+                          "selftest": True, "max_over_ranks": float(t[0]), "gather": gather,
+                          "gather_order_ok": ok}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -281,35 +386,32 @@ def main():
     actions = torch.empty((T, n), dtype=torch.int32, device=device)
     for t in range(T):
         b.synth_actions(args.seed, t, out=actions[t])
-    gather = args.gather and world > 1
-
     def one_step(t):
-        if gather:
-            shard.step_gather(actions[t % T])  # RCCL gather of (obs, reward, term, trunc), pipelined
-        else:
-            b.step(actions[t % T])
+        b.step(actions[t % T])
+
+    def gather_step(t):
+        shard.step_gather(actions[t % T])  # RCCL gather of (obs, reward, term, trunc), pipelined
+
+    def capture(steps):
+        if not steps:
+            return None
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            for k in range(steps):
+                b.step(actions[k % T])
+        torch.cuda.synchronize()
+        return gr
 
     for t in range(args.warmup):
         one_step(t)
-    shard.flush()
     torch.cuda.synchronize()
     K = args.steps
     # graph mode: one graph = `chunk` consecutive pe_step launches; step k of a replay
     # reads action row k % T (plain mode: step t reads row t % T).  K = reps * chunk + rest.
-    chunk = min(args.graph, K) if (args.graph > 1 and not gather) else 0
     pf = b.prefetch_every
-    if chunk > 1 and pf > 0 and chunk % pf:  # every replay must hold the same share of prefetch launches
-        chunk = min(chunk * pf // math.gcd(chunk, pf), max(K, pf))
-    graph = None
-    if chunk > 1:
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            for k in range(chunk):
-                b.step(actions[k % T])
-        torch.cuda.synchronize()
-
-    # with --gather the last gathers are part of the job: waited for inside the window
-    elapsed, kern_ms = timed(torch, dist, device, K, one_step, chunk, graph, shard.flush if gather else None)
+    chunk = plan_graph(K, args.graph, pf)
+    graph = capture(chunk)
+    elapsed, kern_ms = timed(torch, dist, device, K, one_step, chunk, graph)
     b.raise_on_errors()
     total_steps = n * K * world
     value = total_steps / elapsed
@@ -322,14 +424,23 @@ def main():
         Kd = args.desync_steps
         for t in range(200):
             one_step(t)
-        shard.flush()
         torch.cuda.synchronize()
-        d_el, d_kms = timed(torch, dist, device, Kd, one_step, chunk, graph, shard.flush if gather else None)
+        d_chunk = plan_graph(Kd, args.graph, pf)
+        d_graph = graph if d_chunk == chunk else capture(d_chunk)
+        d_el, d_kms = timed(torch, dist, device, Kd, one_step, d_chunk, d_graph)
         d_ach = B * n / (d_kms * 1e-3) / 1e9
         desync = {"value": n * Kd * world / d_el, "unit": "env-steps/s", "steps": Kd,
                   "us_per_step": d_el / Kd * 1e6, "kernel_us": d_kms * 1e3, "achieved": d_ach,
-                  "frac": d_ach / HBM_PEAK_GBPS,
+                  "frac": d_ach / HBM_PEAK_GBPS, "launch": launch_label(Kd, d_chunk),
                   "note": "every env at its own step count in [0, 1000): ~n/1000 auto-resets per step"}
+        b.raise_on_errors()
+
+    # BASELINE config 5's host-boundary leg (gather_leg)
+    gather = None
+    if args.gather_steps > 0:
+        gather = gather_leg(torch, dist, device, shard, args.gather_steps, gather_step, world)
+        gather["episodes"] = "desynchronized (continues the desync window)" if desync is not None else (
+            "as the headline window")
         b.raise_on_errors()
     if rank == 0:
         sha = lib_sha(_capi.LIB_PATH)
@@ -350,10 +461,9 @@ def main():
             "config": {"workload": f"{n} envs/GPU, {G}x{G} grid, {C} rays, range {R}, {plants} plants, "
                                    f"{obstacles} obstacles, auto-reset, actions in HBM",
                        "envs_per_gpu": n, "grid": G, "rays": C, "lidar_range": R,
-                       "parallelism": f"env-shard x{world}" + (" + rccl gather (pipelined)" if gather else ""),
+                       "parallelism": f"env-shard x{world} (independent replicas; RCCL gather leg: 'gather')",
                        "kernel": b.kernel_name,
-                       "launch": f"hipGraph replay, {chunk} pe_step launches per graph" if graph is not None
-                       else "one host launch per step"},
+                       "launch": launch_label(K, chunk)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
                          "bytes_per_env_step": B, "kernel_ms": kern_ms},
@@ -369,6 +479,8 @@ def main():
             out["roofline"]["traffic_note"] = f"no committed PMC profile of this library (lib_sha {sha})"
         if desync is not None:
             out["desync"] = desync
+        if gather is not None:
+            out["gather"] = gather
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, plants, obstacles)
         print(json.dumps(out), flush=True)

@@ -1407,7 +1407,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
 
 // ---------------------------------------------------------------- pe_step_wave
 // The fused step for every geometry without a compile-time sector kernel (any
-// G <= 128, C <= 256, R <= 64; e.g. SURVEY §8(d)'s 64x64 / 64 rays / R=32 stress
+// G <= 128, C <= 120, R <= 64; e.g. SURVEY §8(d)'s 64x64 / 64 rays / R=32 stress
 // variant): ONE WAVE PER ENV.  The rover's window -- grid rows x-R-1 .. x+R+1
 // clipped to the map, one contiguous 16-B-aligned span of the env's block, and
 // visit rows x-3 .. x+3 -- is staged into the wave's LDS region with coalesced
@@ -2482,9 +2482,19 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   g.hstride = (int64_t)align_up((size_t)g.GG, 8);
   // explored words; also the picks scratch of a curriculum reset that keeps visits
   g.estride = (int64_t)align_up((size_t)std::max(g.EW, (P + 1) / 2), 4);
+  // LDS limits: the lane-per-env kernels that every geometry keeps (pe_load_maps_kernel,
+  // and pe_reset_kernel where the cooperative reset does not apply) hold a [64 x D]
+  // obs tile -- this caps C at 120 whatever the step kernel; the one-wave-per-env step
+  // kernel (the step kernel of every geometry without a sector kernel) its header +
+  // 8 per-wave regions.
   if (lds_bytes(g) > 160 * 1024) {
     delete h;
-    return fail(PE_ERR_ARG, "observation tile does not fit LDS");
+    return fail(PE_ERR_ARG, "observation tile does not fit LDS (lidar_channels <= 120)");
+  }
+  if (sizeof(float) * ((size_t)wave_hdr_floats(C, R) + kWaveEnvs * (size_t)wave_lds_floats(G, R, g.WPR, g.NW, g.D)) >
+      160 * 1024) {
+    delete h;
+    return fail(PE_ERR_ARG, "the one-wave-per-env step kernel's window does not fit LDS");
   }
 
   Rules& rl = h->rl;

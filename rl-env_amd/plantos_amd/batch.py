@@ -169,6 +169,11 @@ class PlantOSBatch:
         stream (graph-capturable); the library binds and restores the device.
         io: another output buffer (new_io()) to write this step's outputs to."""
         if io is not None:
+            if not (type(io) is torch.Tensor and io.dtype is torch.uint8 and io.is_cuda
+                    and io.get_device() == self._dev_index and io.is_contiguous()
+                    and io.numel() == self.io_bytes()):
+                raise ValueError(f"io must be a contiguous uint8 tensor of {self.io_bytes()} bytes on {self.device} "
+                                 "(PlantOSBatch.new_io())")
             o, r_, te_, tr_ = self.io_views(io)
             rc = self._L.pe_step(self.handle, self._actions_ptr(actions), self._act_bytes, o.data_ptr(),
                                  r_.data_ptr(), te_.data_ptr(), tr_.data_ptr(),

@@ -38,26 +38,37 @@ class ShardedPlantOS:
             batch_factory = lambda n, **kw: PlantOSBatch(n, device=dev, **cfg, **kw)  # noqa: E731
         self.batch = batch_factory(self.n, env_id_offset=lo, seed=seed)
         self._slots = None
+        self._last_io = None  # the buffer the latest step wrote (None: the batch's own io)
 
     @property
     def device(self):
         return self.batch.device
 
     def step(self, actions_local):
+        self._last_io = None
         return self.batch.step(actions_local)
 
-    def _pack(self, outs):
-        """One step's outputs of this shard as ONE flat u8 buffer (the batch's io
-        buffer itself when it has one: no copy)."""
+    def io_bytes(self):
+        """Bytes of one rank's packed step outputs (what one gather moves per rank)."""
+        return 4 * self.n * self.batch.obs_dim + 6 * self.n
+
+    def _pack(self):
+        """The latest step's outputs of this shard as ONE flat u8 buffer: the buffer
+        that step wrote (the batch's io, or step_gather's slot) -- no copy."""
+        if self._last_io is not None:
+            return self._last_io
         io = getattr(self.batch, "io", None)
         if io is not None:
             return io
-        return torch.cat([t.contiguous().view(-1).view(torch.uint8) for t in outs])
+        b = self.batch
+        return torch.cat([t.contiguous().view(-1).view(torch.uint8)
+                          for t in (b.obs, b.reward, b.terminated, b.truncated)])
 
-    def _unpack(self, flats, like):
-        """Concatenate the W ranks' flat buffers into global (obs, reward, term, trunc)."""
+    def unpack(self, flats):
+        """The W ranks' packed buffers (rank order, e.g. ``gathered(slot)``) as the
+        global (obs f32 [W*n, D], reward f32 [W*n], terminated u8, truncated u8)."""
         n = self.n
-        D = like[0].shape[1]
+        D = self.batch.obs_dim
         sizes = (4 * n * D, 4 * n, n, n)
         parts = [[], [], [], []]
         for f in flats:
@@ -72,16 +83,14 @@ class ShardedPlantOS:
         """(obs, reward, terminated, truncated) of all ranks, concatenated in global
         env order on `root` (None elsewhere): ONE gather of each rank's packed
         output buffer (RCCL over xGMI on GPUs)."""
-        b = self.batch
-        outs = (b.obs, b.reward, b.terminated, b.truncated)
+        flat = self._pack()
         if self.world == 1:
-            return outs
-        flat = self._pack(outs)
+            return self.unpack([flat])
         lst = [torch.empty_like(flat) for _ in range(self.world)] if self.rank == root else None
         dist.gather(flat, lst, dst=root, group=self.group)
         if self.rank != root:
             return None
-        return self._unpack(lst, outs)
+        return self.unpack(lst)
 
     def step_gather(self, actions_local, root=0):
         """Pipelined step + host-boundary gather (GPU batches): the step writes into
@@ -89,33 +98,47 @@ class ShardedPlantOS:
         so the gather of step t overlaps step t+1; before a buffer is written again
         the stream waits for its previous gather.  Returns the slot used; the
         gathered buffers of a slot are `gathered(slot)` on root once `flush()` (or
-        the slot's next use) has waited for it."""
+        the slot's next use) has waited for it; `unpack(gathered(slot))` gives the
+        global (obs, reward, terminated, truncated).  With one rank nothing is
+        gathered: `gathered(slot)` is the slot itself."""
         b = self.batch
         if self._slots is None:
             self._slots = [b.new_io(), b.new_io()]
-            self._glist = [[torch.empty_like(self._slots[k]) for _ in range(self.world)] if self.rank == root
-                           else None for k in range(2)]
+            self._glist = [[torch.empty_like(self._slots[k]) for _ in range(self.world)]
+                           if (self.rank == root and self.world > 1) else None for k in range(2)]
             self._work = [None, None]
+            self._root = root
             self._k = 0
         k = self._k
         self._k ^= 1
         if self._work[k] is not None:
             self._work[k].wait()  # the stream waits for the slot's previous gather
+            self._work[k] = None
         b.step(actions_local, io=self._slots[k])
+        self._last_io = self._slots[k]
         if self.world > 1:
             self._work[k] = dist.gather(self._slots[k], self._glist[k], dst=root, group=self.group, async_op=True)
         return k
 
     def gathered(self, k):
+        """Root: the W ranks' packed buffers of slot k (rank order); None elsewhere."""
+        if self._slots is None:
+            raise ValueError("no step_gather yet")
+        if self.world == 1:
+            return [self._slots[k]]
         return self._glist[k]
+
+    def wait(self, k):
+        """Wait for slot k's gather only (the other slot's may stay in flight)."""
+        if self._slots is not None and self._work[k] is not None:
+            self._work[k].wait()
+            self._work[k] = None
 
     def flush(self):
         if self._slots is None:
             return
         for k in range(2):
-            if self._work[k] is not None:
-                self._work[k].wait()
-                self._work[k] = None
+            self.wait(k)
 
     def scatter_actions(self, actions_global=None, root=0):
         """Root's global action vector -> this rank's shard (int64 [n])."""

@@ -25,6 +25,7 @@ CFG = {
     "g25r4": (25, 10, 12, 4, 16),  # multi-word C16R4
     "g12r2": (12, 4, 6, 2, 10),    # one-word C10R2 (g21 = the constructor default: multi-word C10R2)
     "g8r12": (8, 3, 3, 12, 16),    # R > G: the wave kernel's raw-window ray path (no rover-aligned re-staging)
+    "g24c100": (24, 10, 12, 8, 100),  # C = 100 (near the 120-ray LDS bound): wave kernel, rays past lane 63
 }
 
 # which step kernel each geometry runs (pe_kernel_name): the sector kernel wherever a
@@ -33,7 +34,7 @@ KERNELS = {
     "g20": "pe_step_quad<C16,R6,1word>", "g25": "pe_step_quad<C16,R6>", "g64": "pe_step_quad<C64,R6>",
     "g21": "pe_step_quad<C10,R2>", "g12r2": "pe_step_quad<C10,R2,1word>", "g15": "pe_step_quad<C16,R4,1word>",
     "g25r4": "pe_step_quad<C16,R4>", "g64r32": "pe_step_wave", "g7": "pe_step_wave",
-    "g32": "pe_step_wave", "g8r12": "pe_step_wave",
+    "g32": "pe_step_wave", "g8r12": "pe_step_wave", "g24c100": "pe_step_wave",
 }
 
 
@@ -159,7 +160,7 @@ def test_kernel_selection(name):
 @pytest.mark.parametrize("name,n,steps", [("g20", 4096, 1100), ("g21", 1000, 1010), ("g7", 777, 400),
                                           ("g64", 256, 120), ("g64r32", 96, 60), ("g25", 300, 200),
                                           ("g15", 1000, 1010), ("g25r4", 300, 200), ("g12r2", 500, 300),
-                                          ("g32", 400, 300), ("g8r12", 300, 300)])
+                                          ("g32", 400, 300), ("g8r12", 300, 300), ("g24c100", 200, 120)])
 def test_rollout_parity_device_rng(name, n, steps):
     """Device-rng episodes with synthetic actions, auto-reset included (g20 crosses
     the 1000-step truncation): every output of every step vs the oracle."""
@@ -192,10 +193,11 @@ def test_rollout_parity_device_rng(name, n, steps):
 
 
 @pytest.mark.parametrize("name,desync", [("g20", False), ("g20", True), ("g64", False), ("g64", True),
-                                         ("g64r32", True)])
+                                         ("g64r32", True), ("g25", False), ("g25", True)])
 def test_full_batch_sampled_parity_and_invariants(name, desync):
-    """65536 envs (BASELINE headline 20x20/16 rays and the 64x64/64-ray stress
-    config) for 1010+ steps, crossing the 1000-step truncation: the oracle replays
+    """65536 envs (BASELINE headline 20x20/16 rays, the 64x64/64-ray stress config,
+    and 25x25/16 rays -- the geometry the reference's training scripts build,
+    A2C_training.py:206-212, trainingCode.py:121-125) for 1010+ steps, crossing the 1000-step truncation: the oracle replays
     192 sampled global env ids (envs are independent) every step, and size-
     independent invariants hold over ALL envs (one-hot per ray, distances in {r/R},
     positions in {x/G}, slice values in {k/10}, episode counts and step counts
@@ -300,6 +302,17 @@ def test_out_of_range_actions():
     s = np_(b.get_state()["scalars"])
     assert (s == ov.b.scal).all()
     b.close()
+
+
+def test_lds_bounds_of_the_ray_count():
+    """lidar_channels beyond the LDS obs tile of the lane-per-env reset / load_maps
+    kernels (C > 120) is refused at create, not launched"""
+    from plantos_amd import PlantOSBatch
+    with pytest.raises(ValueError, match="LDS"):
+        PlantOSBatch(8, grid_size=20, num_plants=10, num_obstacles=12, lidar_range=6, lidar_channels=200,
+                     device="cuda:0")
+    PlantOSBatch(8, grid_size=20, num_plants=10, num_obstacles=12, lidar_range=6, lidar_channels=120,
+                 device="cuda:0").close()
 
 
 def test_no_room_raises():

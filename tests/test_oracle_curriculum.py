@@ -33,6 +33,10 @@ class OracleCurriculumVec:
         self.completed = np.zeros(n, bool)
         self.persistent = [None] * n
 
+    def _new_map(self, e):
+        """plantos_env.py:125-158 on the shared CPython stream (DummyVecEnv order)."""
+        self.b.reset_cpython(e, self.mt)
+
     def reset_env(self, e):
         self.episodes[e] += 1
         self.on_maze[e] += 1
@@ -43,11 +47,11 @@ class OracleCurriculumVec:
                 self.successes[e] += 1
             self.completed[e] = False
             self.on_maze[e] = 0
-            self.b.reset_cpython(e, self.mt)
+            self._new_map(e)
             obs = self.b.obs([e])[e]
             self.persistent[e] = None
         else:
-            self.b.reset_cpython(e, self.mt)
+            self._new_map(e)
             obs = self.b.obs([e])[e]  # computed before the injection below
             if self.persistent[e] is not None:
                 self.b.visits[e] = self.persistent[e].copy()

@@ -22,6 +22,8 @@ def _free_port():
 
 
 def _worker(rank, world, port, n, steps, q, pipelined=False):
+    """pipelined: step t+1's gather is issued before step t's result is checked (only
+    step t's slot is waited for), so two gathers are in flight at once."""
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     repo = os.path.dirname(here)
@@ -47,34 +49,54 @@ def _worker(rank, world, port, n, steps, q, pipelined=False):
         full = OracleVec(CFG, np.arange(world * n), 9, max_steps=25) if rank == 0 else None
         rng = np.random.default_rng(0)
         ok = True
+        expect = []  # rank 0: the single-batch oracle's outputs of steps not checked yet
+
+        def check(g):
+            obs, rew, te, tr = expect.pop(0)
+            good = bool((g[0].numpy() == obs).all() and (g[1].numpy() == rew.astype(np.float32)).all())
+            return good and bool((g[2].numpy().astype(bool) == te).all() and (g[3].numpy().astype(bool) == tr).all())
+
+        prev = None
         for t in range(steps):
             a_glob = torch.as_tensor(rng.integers(0, 5, world * n))
             a_loc = sh.scatter_actions(a_glob if rank == 0 else None)
             assert (a_loc.numpy() == a_glob.numpy()[rank * n:(rank + 1) * n]).all()
+            if rank == 0:
+                expect.append(full.step(a_glob.numpy())[:4])
             if pipelined:
                 k = sh.step_gather(a_loc)
-                sh.flush()
-                g = sh._unpack(sh.gathered(k), sh.batch.io_views(sh._slots[k])) if rank == 0 else None
+                if prev is not None:  # step t-1's gather: waited for while step t's is in flight
+                    sh.wait(prev)
+                    if rank == 0:
+                        ok &= check(sh.unpack(sh.gathered(prev)))
+                prev = k
             else:
                 sh.step(a_loc)
                 g = sh.gather_outputs()
+                if rank == 0:
+                    ok &= check(g)
+                else:
+                    assert g is None
+        if pipelined:
+            sh.flush()
             if rank == 0:
-                obs, rew, te, tr, *_ = full.step(a_glob.numpy())
-                ok &= bool((g[0].numpy() == obs).all() and (g[1].numpy() == rew.astype(np.float32)).all())
-                ok &= bool((g[2].numpy().astype(bool) == te).all() and (g[3].numpy().astype(bool) == tr).all())
-            else:
-                assert g is None
+                ok &= check(sh.unpack(sh.gathered(prev)))
+                # gather_outputs after step_gather gathers the slot the last step wrote
+            g = sh.gather_outputs()
+            if rank == 0:
+                ok &= bool((g[0] == sh.unpack(sh.gathered(prev))[0]).all())
         if rank == 0:
+            ok &= not expect
             q.put(ok)
     finally:
         dist.destroy_process_group()
 
 
-def _run(pipelined):
+def _run(pipelined, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, 6, 40, q, pipelined)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 6, 40, q, pipelined)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -92,3 +114,10 @@ def test_pipelined_step_gather_equals_one_batch():
     """step_gather: double-buffered outputs, each step's gather issued asynchronously
     and waited for only before its buffer is written again (flush at the end)"""
     _run(True)
+
+
+def test_single_rank_step_gather_and_gather_outputs():
+    """world 1: step_gather issues no collective; gathered(slot) is the slot itself
+    (never an uninitialized buffer) and gather_outputs returns the latest step's"""
+    _run(True, world=1)
+    _run(False, world=1)

@@ -5,6 +5,7 @@
 #   usage: bash tools/gpu_session.sh TAG step [step ...]
 #   steps: tests | smoke | bench | benchd | bench64 | stats | statsd | stats64 |
 #          pmcf | pmcw | pmcf64 | pmcw64 | stamps | stampsd | benchx:<name>:<args> | statsx:<name>:<args> |
+#          pmcx:<name>:<FETCH_SIZE|WRITE_SIZE>:<bench args with _ for spaces> |
 #          ab:<name>:<rounds>:<lib,lib,...>:<bench args with _ for spaces>
 set -euo pipefail
 TAG=$1
@@ -12,7 +13,7 @@ shift
 OUT=gpurun_out
 mkdir -p $OUT
 export TMPDIR=/tmp
-HEAD_ARGS="--steps 4096 --warmup 200 --desync-steps 0 --no-cpu-baseline"
+HEAD_ARGS="--steps 4096 --warmup 200 --desync-steps 0 --gather-steps 0 --no-cpu-baseline"
 for w in "$@"; do
   case $w in
     tests)
@@ -22,7 +23,7 @@ for w in "$@"; do
     bench)
       timeout -k 10 300 python bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err ;;
     benchd)
-      timeout -k 10 300 python bench.py --desync --steps 20480 --warmup 200 --desync-steps 0 --no-cpu-baseline \
+      timeout -k 10 300 python bench.py --desync --steps 20480 --warmup 200 --desync-steps 0 --gather-steps 0 --no-cpu-baseline \
         > $OUT/benchd_$TAG.json 2> $OUT/benchd_$TAG.err ;;
     bench64)
       timeout -k 10 300 python bench.py --grid 64 --rays 64 --range 6 --steps 3000 --warmup 100 --desync-steps 3000 \
@@ -32,17 +33,17 @@ for w in "$@"; do
         python3 bench.py $HEAD_ARGS > $OUT/stats_bench_$TAG.json 2> $OUT/stats_$TAG.err ;;
     statsd)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/statsd_$TAG -o run -- \
-        python3 bench.py --desync --steps 20480 --warmup 200 --desync-steps 0 --no-cpu-baseline \
+        python3 bench.py --desync --steps 20480 --warmup 200 --desync-steps 0 --gather-steps 0 --no-cpu-baseline \
         > $OUT/statsd_bench_$TAG.json 2> $OUT/statsd_$TAG.err ;;
     stats64)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/stats64_$TAG -o run -- \
-        python3 bench.py --grid 64 --rays 64 --range 6 --steps 2000 --warmup 100 --desync-steps 0 --no-cpu-baseline \
+        python3 bench.py --grid 64 --rays 64 --range 6 --steps 2000 --warmup 100 --desync-steps 0 --gather-steps 0 --no-cpu-baseline \
         > $OUT/stats64_bench_$TAG.json 2> $OUT/stats64_$TAG.err ;;
     pmcf|pmcw|pmcf64|pmcw64)
       ctr=FETCH_SIZE; [[ $w == pmcw* ]] && ctr=WRITE_SIZE
       geo=""; [[ $w == *64 ]] && geo="--grid 64 --rays 64 --range 6"
       timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace -f csv -d $OUT/${w}_$TAG -o run -- \
-        python3 bench.py $geo --steps 50 --warmup 10 --desync-steps 0 --no-cpu-baseline \
+        python3 bench.py $geo --steps 50 --warmup 10 --desync-steps 0 --gather-steps 0 --no-cpu-baseline \
         > $OUT/${w}_$TAG.json 2> $OUT/${w}_$TAG.err ;;
     stamps|stampsd)
       flag=""; [ $w = stampsd ] && flag="--desync"
@@ -54,6 +55,11 @@ for w in "$@"; do
       IFS=: read -r _ name args <<< "$w"
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/statsx_${name}_$TAG -o run -- \
         python3 bench.py ${args//_/ } > $OUT/statsx_${name}_$TAG.json 2> $OUT/statsx_${name}_$TAG.err ;;
+    pmcx:*)  # one PMC pass (one counter) over a short bench run of the given geometry
+      IFS=: read -r _ name ctr args <<< "$w"
+      timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace -f csv -d $OUT/pmcx_${name}_${ctr}_$TAG -o run -- \
+        python3 bench.py ${args//_/ } --steps 50 --warmup 10 --desync-steps 0 --gather-steps 0 --no-cpu-baseline \
+        > $OUT/pmcx_${name}_${ctr}_$TAG.json 2> $OUT/pmcx_${name}_${ctr}_$TAG.err ;;
     ab:*)
       IFS=: read -r _ name rounds libs args <<< "$w"
       libs=${libs//,/ }  # lib[+VAR=VAL]: ab_bench.sh's lib,VAR=VAL
