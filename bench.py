@@ -224,8 +224,10 @@ def timed(torch, dist, device, K, one_step, chunk, graph, finish=None):
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(device)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # HIP events on the stream pe_step launches on; the opening one is recorded before
+    # the wall clock starts (its host-side cost, ~10 us on ROCm, is instrumentation)
+    ev0.record(stream)
     t0 = time.perf_counter()
-    ev0.record(stream)  # HIP events on the stream pe_step launches on
     if graph is not None:
         for _ in range(K // chunk):
             graph.replay()
@@ -238,10 +240,10 @@ def timed(torch, dist, device, K, one_step, chunk, graph, finish=None):
         finish()
     ev1.record(stream)
     torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0  # this rank's K steps; the job's time is the max over ranks
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+        torch.cuda.synchronize()
     kern_ms = ev0.elapsed_time(ev1) / K
     if dist:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=device)

@@ -17,9 +17,11 @@ struct pe_handle {
   int tile_codes;    // the sector kernel's obs tile holds byte codes (pe_step_quad<..., BT>); so do the
                      // prefetched records' obs rows
   const char* kname;
+  char kname_buf[64];  // kname with the envs-per-workgroup suffix (small batches)
   void* cur_mem;     // CurriculumWrapper records (pe_curriculum_enable), or NULL
   size_t lds_floor;  // minimum dynamic LDS per step workgroup (PE_LDS_FLOOR, debug builds only)
   int quad_waves;    // waves per workgroup of the sector kernel (4; 8 via PE_QUAD_WAVES in debug builds)
+  int quad_epb;      // envs per workgroup of the sector kernel (64; 16 / 32 for small batches, C16R6 one-word)
   int stagger;       // sector-kernel start delay per block quarter (PE_STAGGER, debug builds only)
   int coop_max_done; // wave-cooperative auto-resets up to this many done envs per block (pe_coop.hpp;
                      // pe_config.coop_max_done)

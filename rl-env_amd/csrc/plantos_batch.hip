@@ -603,7 +603,9 @@ template <int NW, bool ONEWORD, int KD, bool BT = false>  // one copy per kernel
 __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, int C, int R, int lane, int wv, int CW,
                                                 int64_t e0, bool done, uint4 sp, double ret, int ndone, bool wfix,
                                                 const float* ctab = nullptr, const float* stage = nullptr,
-                                                bool stage_info = false) {
+                                                bool stage_info = false, int64_t e_early = -1,
+                                                const PfLoad<ONEWORD ? 1 : kCoopWPR, KD>* early = nullptr,
+                                                const Row4<ONEWORD ? 1 : kCoopWPR>* early_rows = nullptr) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const StepArgs& a = *reinterpret_cast<const StepArgs*>(ka);
   const Geo& g = a.g;
@@ -644,57 +646,97 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
       const int l = __ffsll((unsigned long long)dmw) - 1;
       const int64_t el = e0 + l;
       OT* orow = rows + l * g.D;
-      // the record: staged into LDS before the done barrier (stage), or loaded now
-      PfLoad<MAXW, KD> pl;
-      if (a.pf.scal && !stage) coop_load_prefetched<MAXW, KD>(a.pf, g, el, pl, lane);  // in flight from here on
-      bool keep = false;
-      if (done && st.cur) keep = curriculum_on_reset(st.cur, e, rl);  // A2C_training.py:56-95
-      const bool kp = __builtin_amdgcn_readlane((int)keep, l) != 0;
-      const int wf = __builtin_amdgcn_readlane((int)wfix, l);
-      const Scal sv = unpack(make_uint4((uint32_t)__builtin_amdgcn_readlane((int)sp.x, l),
-                                        (uint32_t)__builtin_amdgcn_readlane((int)sp.y, l),
-                                        (uint32_t)__builtin_amdgcn_readlane((int)sp.z, l),
-                                        (uint32_t)__builtin_amdgcn_readlane((int)sp.w, l)));
-      if (a.tobs) {
-        float* t = a.tobs + el * g.D;
-        for (int k2 = lane; k2 < g.D; k2 += 64) t[k2] = tval(orow, k2);
-      }
-      // with the curriculum the commit stored this env's rows: they must land before
-      // the info reads them and the reset rewrites them
-      if (st.cur || stage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (stage: the LDS-DMA landed)
-      PE_DSTAMP(1);
-      if (a.tinfo) {
-        if (stage_info)  // the env's rows came with the record
-          coop_info_store<MAXW>(st, g,
-                                pf_stage_rows<MAXW>(reinterpret_cast<const uint64_t*>(
-                                                        stage + 4 + 4 * pf_grid_units(g.G, g.WPR) + a.pf.ostride / 4),
-                                                    g, lane),
-                                sv, a.tinfo + el * PE_NINFO, lane, wf, ltab);
-        else
-          coop_write_info<MAXW>(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, wf);
-      }
-      PE_DSTAMP(2);
-      Row4<MAXW> rw;
-      Scal ns;
-      asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
-      const bool took = stage ? pf_stage_take<MAXW>(stage, g, (int)a.pf.ostride, sv.episode, rw, ns, orow, lane)
-                              : (a.pf.scal && take(el, sv.episode, pl, rw, ns, orow));
-      if (took) {
-        ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane);
+      // early: the kernel loaded this env's record and rows behind the compute phase
+      const bool early_hit = !BT && KD <= 2 && early != nullptr && el == e_early;
+      if (early_hit) {
+        // the record and the env's rows were loaded behind the compute phase (the
+        // kernel's early record): every wait here is for loads issued ~1 us ago.
+        // Terminal obs held in registers while the fresh row replaces it in the tile;
+        // stores only after every load is consumed.
+        const int wf = __builtin_amdgcn_readlane((int)wfix, l);
+        const Scal sv = unpack(make_uint4((uint32_t)__builtin_amdgcn_readlane((int)sp.x, l),
+                                          (uint32_t)__builtin_amdgcn_readlane((int)sp.y, l),
+                                          (uint32_t)__builtin_amdgcn_readlane((int)sp.z, l),
+                                          (uint32_t)__builtin_amdgcn_readlane((int)sp.w, l)));
+        float tv[KD];
+#pragma unroll
+        for (int j = 0; j < KD; ++j) tv[j] = lane + 64 * j < g.D ? tval(orow, lane + 64 * j) : 0.0f;
+        if (a.tinfo) coop_info_store<MAXW>(st, g, *early_rows, sv, a.tinfo + el * PE_NINFO, lane, wf, ltab);
+        Row4<MAXW> rw;
+        Scal ns;
+        asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
+        if (take(el, sv.episode, *early, rw, ns, orow)) {
+          ns = coop_apply_reset<MAXW>(st, g, el, ns, false, rw, lane);
+        } else {  // the record is not this reset's (not generated yet): generate in place
+          uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
+          ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, false, rw, lane, scr);
+          coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
+        }
+        if (a.tobs) {
+          float* t = a.tobs + el * g.D;
+#pragma unroll
+          for (int j = 0; j < KD; ++j)
+            if (lane + 64 * j < g.D) t[lane + 64 * j] = tv[j];
+        }
+        if (lane == 0) a.pf.flag[el] = 1;  // its next map goes into the next generating batch
+        if (done) {  // lane l: program order after its commit stores
+          s = ns;
+          st.ep_ret[e] = 0.0;
+          st.scal[e] = pack(s);
+        }
       } else {
-        uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
-        ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane, scr);
-        coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
+        // the record: staged into LDS before the done barrier (stage), or loaded now
+        PfLoad<MAXW, KD> pl;
+        if (a.pf.scal && !stage) coop_load_prefetched<MAXW, KD>(a.pf, g, el, pl, lane);  // in flight from here on
+        bool keep = false;
+        if (done && st.cur) keep = curriculum_on_reset(st.cur, e, rl);  // A2C_training.py:56-95
+        const bool kp = __builtin_amdgcn_readlane((int)keep, l) != 0;
+        const int wf = __builtin_amdgcn_readlane((int)wfix, l);
+        const Scal sv = unpack(make_uint4((uint32_t)__builtin_amdgcn_readlane((int)sp.x, l),
+                                          (uint32_t)__builtin_amdgcn_readlane((int)sp.y, l),
+                                          (uint32_t)__builtin_amdgcn_readlane((int)sp.z, l),
+                                          (uint32_t)__builtin_amdgcn_readlane((int)sp.w, l)));
+        if (a.tobs) {
+          float* t = a.tobs + el * g.D;
+          for (int k2 = lane; k2 < g.D; k2 += 64) t[k2] = tval(orow, k2);
+        }
+        // with the curriculum the commit stored this env's rows: they must land before
+        // the info reads them and the reset rewrites them
+        if (st.cur || stage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (stage: the LDS-DMA landed)
+        PE_DSTAMP(1);
+        if (a.tinfo) {
+          if (stage_info)  // the env's rows came with the record
+            coop_info_store<MAXW>(st, g,
+                                  pf_stage_rows<MAXW>(reinterpret_cast<const uint64_t*>(
+                                                          stage + 4 + 4 * pf_grid_units(g.G, g.WPR) + a.pf.ostride / 4),
+                                                      g, lane),
+                                  sv, a.tinfo + el * PE_NINFO, lane, wf, ltab);
+          else
+            coop_write_info<MAXW>(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, wf);
+        }
+        PE_DSTAMP(2);
+        Row4<MAXW> rw;
+        Scal ns;
+        asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
+        const bool took = stage ? pf_stage_take<MAXW>(stage, g, (int)a.pf.ostride, sv.episode, rw, ns, orow, lane)
+                                : (a.pf.scal && take(el, sv.episode, pl, rw, ns, orow));
+        if (took) {
+          ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane);
+        } else {
+          uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
+          ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane, scr);
+          coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
+        }
+        PE_DSTAMP(3);
+        if (a.pf.scal && lane == 0) a.pf.flag[el] = 1;  // its next map goes into the next generating batch
+        PE_DSTAMP(4);
+        if (done) {  // lane l: program order after its commit stores
+          s = ns;
+          st.ep_ret[e] = 0.0;
+          st.scal[e] = pack(s);
+        }
+        PE_DSTAMP(5);
       }
-      PE_DSTAMP(3);
-      if (a.pf.scal && lane == 0) a.pf.flag[el] = 1;  // its next map goes into the next generating batch
-      PE_DSTAMP(4);
-      if (done) {  // lane l: program order after its commit stores
-        s = ns;
-        st.ep_ret[e] = 0.0;
-        st.scal[e] = pack(s);
-      }
-      PE_DSTAMP(5);
     }
     __syncthreads();  // the fresh obs row is in the tile
     __builtin_amdgcn_s_waitcnt(0x0F70);  // see the end of the path below
@@ -851,9 +893,14 @@ __device__ __forceinline__ void quad_done_obs(const void* ka, int tile_off, int 
 // BT: byte-coded obs tile (pe_coop.hpp ObsW<uint8_t>): [64 x D] bytes instead of
 // floats in LDS (64x64 / 64 rays: 22 KB instead of 89 KB), expanded through the LDS
 // code table at the tile store -- the f32 tile held the kernel to one workgroup per CU.
-template <int C, int R, bool ONEWORD, int NW, bool BT = false>
+// EPB: envs per workgroup (64; 16 / 32 for small batches: more workgroups, so that
+// a batch of a few thousand envs spreads over every CU -- lanes >= EPB idle).  The
+// LDS layout keeps the 64-env stride LS whatever EPB.
+template <int C, int R, bool ONEWORD, int NW, bool BT = false, int EPB = kQuadEnvs>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs; NW=4: <= 128 VGPRs (4 workgroups per CU: G=25 13.1 -> 10.5 us; 1-word C16: 122 -> 104 VGPRs)
-  constexpr int NR = 2 * R + 3, NV = 7, EPB = kQuadEnvs, CW = NW - 1;  // CW: commit wave
+  constexpr int NR = 2 * R + 3, NV = 7, LS = kQuadEnvs, CW = NW - 1;  // CW: commit wave
+  static_assert(EPB == 16 || EPB == 32 || EPB == 64, "envs per workgroup");
+  static_assert(!BT || EPB == kQuadEnvs, "the byte-coded kernel's LDS-DMA staging predicts over all 64 lanes");
 
   static_assert(C >= NW, "every wave owns a sector of at least one ray");
   static_assert(ONEWORD || R <= 14, "funnel-shifted window row must hold 2R+5 cells");
@@ -862,10 +909,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   float* tdist = smem;
   float* tpos = smem + 72;
   float* tvis = smem + 328;
-  uint64_t* lrow = reinterpret_cast<uint64_t*>(smem + kTabFloats);  // [NR][EPB]
-  uint32_t* lvis = reinterpret_cast<uint32_t*>(lrow + NR * EPB);    // [NV][EPB]
+  uint64_t* lrow = reinterpret_cast<uint64_t*>(smem + kTabFloats);  // [NR][LS]
+  uint32_t* lvis = reinterpret_cast<uint32_t*>(lrow + NR * LS);    // [NV][LS]
   using OT = typename std::conditional<BT, uint8_t, float>::type;
-  OT* rows = reinterpret_cast<OT*>(smem + quad_tile_off<R>());     // [EPB][D] floats or codes
+  OT* rows = reinterpret_cast<OT*>(smem + quad_tile_off<R>());     // [LS][D] floats or codes
   float* ctab = smem + quad_ctab_off<R, C>();                       // BT: code -> float
   const Geo& g = a.g;
   const Rules& rl = a.rl;
@@ -874,17 +921,17 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int64_t e0 = (int64_t)blockIdx.x * EPB;
   const int64_t e = e0 + lane;
-  const bool live = e < a.n;
+  const bool live = (EPB == LS || lane < EPB) && e < a.n;
 
   // ---- round 1: env-indexed loads (all waves).  Every thread also plays a LOADER
-  // role for round 2: LT = NW threads per env (env le, part sub), so each load
-  // instruction reads LT consecutive rows of 64/LT envs instead of one row of 64.
+  // role for round 2: LT = 64 NW / EPB threads per env (env le < EPB, part sub), so
+  // each load instruction reads LT consecutive rows of 64/LT envs instead of one row of 64.
   PE_STAMP(0);
   if (a.stagger) {  // de-phase the resident workgroups of a CU (speed only)
     const int q = (int)(blockIdx.x * PE_STAGGER_GROUPS / gridDim.x);
     for (int i = 0; i < q * a.stagger; ++i) __builtin_amdgcn_s_sleep(8);
   }
-  constexpr int LT = NW;
+  constexpr int LT = NW * (LS / EPB);
   const int le = threadIdx.x / LT, sub = threadIdx.x % LT;
   const int64_t el = e0 + le;
   const bool llive = el < a.n;
@@ -902,7 +949,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   // one-word rows (G <= 20): the loader env's whole grid block (gstride / 2 <= 10
   // 16-B units, contiguous, 3 per loader thread) comes in round 1 -- its address does
   // not depend on the position -- and only the visit rows are left for round 2
-  constexpr int JG1 = 3;
+  constexpr int JG1 = (10 + LT - 1) / LT;  // gstride / 2 <= 10 16-B units (G <= 20)
   constexpr bool kGridR1 = ONEWORD && PE_GRID_R1;
   uint4 qg1[kGridR1 ? JG1 : 1];
   if constexpr (kGridR1) {
@@ -984,7 +1031,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   // only (64x64 desynchronized: 36.6 -> 36.2 us): at 20x20 the waits hipcc places
   // around a possibly outstanding LDS-DMA (a vmcnt(0) at the next use of any load
   // result) serialize round 2 in every block (9.39 -> 10.0 us, desync 11.52 -> 12.29).
-  float* stage = smem + (BT ? quad_ctab_off<R, C>() + 256 : quad_tile_off<R>() + EPB * (5 * C + 27));
+  float* stage = smem + (BT ? quad_ctab_off<R, C>() + 256 : quad_tile_off<R>() + LS * (5 * C + 27));
   const bool stage_ok = BT && a.pf.scal && quad_coop(a, 1) && e0 + EPB <= a.n;  // full block: every lane live
   const bool stage_info = !st.cur && a.tinfo && pf_stage_info_fits(g.G, g.WPR, (int)a.pf.ostride);
   // (issued right after round 2's own loads: hipcc drains every memory op in flight
@@ -1051,14 +1098,14 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
           if (q < nq) {
             const uint64_t lo = (uint64_t)qg1[j].x | ((uint64_t)qg1[j].y << 32);
             const uint64_t hi = (uint64_t)qg1[j].z | ((uint64_t)qg1[j].w << 32);
-            if (ka >= 0 && ka < NR) lrow[ka * EPB + le] = lo;
-            if (ka + 1 >= 0 && ka + 1 < NR && 2 * q + 1 < g.G) lrow[(ka + 1) * EPB + le] = hi;
+            if (ka >= 0 && ka < NR) lrow[ka * LS + le] = lo;
+            if (ka + 1 >= 0 && ka + 1 < NR && 2 * q + 1 < g.G) lrow[(ka + 1) * LS + le] = hi;
           }
         }
 #pragma unroll
         for (int j = 0; j < (NR + LT - 1) / LT; ++j) {
           const int k = sub + LT * j, xr = base + k;
-          if (k < NR && (xr < 0 || xr >= g.G)) lrow[k * EPB + le] = kEven64;  // off-map rows: obstacles
+          if (k < NR && (xr < 0 || xr >= g.G)) lrow[k * LS + le] = kEven64;  // off-map rows: obstacles
         }
       }
 #pragma unroll
@@ -1073,8 +1120,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
           const uint64_t va = (ra >= 0 && ra < g.G) ? (ra == rc ? lo : hi) : kEven64;
           const uint64_t vb2 = (ra + 1 >= 0 && ra + 1 < g.G) ? (ra + 1 == rc ? lo : hi) : kEven64;
           const int ka = ra - base;
-          if (ka >= 0 && ka < NR) lrow[ka * EPB + le] = va;
-          if (ka + 1 >= 0 && ka + 1 < NR) lrow[(ka + 1) * EPB + le] = vb2;
+          if (ka >= 0 && ka < NR) lrow[ka * LS + le] = va;
+          if (ka + 1 >= 0 && ka + 1 < NR) lrow[(ka + 1) * LS + le] = vb2;
         }
       }
       // visit rows: one 16-B row per load, funnel-shifted to ybv
@@ -1089,13 +1136,13 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
             const uint4 q = qv1[j];
             const uint32_t lo = vw == 0 ? q.x : (vw == 1 ? q.y : q.z);
             const uint32_t hi = vw == 0 ? q.y : (vw == 1 ? q.z : q.w);
-            lvis[k * EPB + le] = vo ? ((lo >> vo) | (hi << (32 - vo))) : lo;
+            lvis[k * LS + le] = vo ? ((lo >> vo) | (hi << (32 - vo))) : lo;
           }
         }
 #pragma unroll
         for (int j = 0; j < JV; ++j) {
           const int k = sub + LT * j, xr = lx - 3 + k;
-          if (k < NV && (xr < 0 || xr >= g.G)) lvis[k * EPB + le] = 0xAAAAAAAAu;
+          if (k < NV && (xr < 0 || xr >= g.G)) lvis[k * LS + le] = 0xAAAAAAAAu;
         }
       }
 #pragma unroll
@@ -1107,7 +1154,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
 #pragma unroll
             for (int i = 0; i < JX; ++i) acc ^= qx[i].x ^ qx[i].y ^ qx[i].z ^ qx[i].w;
           }
-          lvis[k * EPB + le] = acc == 0x9E3779B9u ? 0x22222222u : 0x11111111u;
+          lvis[k * LS + le] = acc == 0x9E3779B9u ? 0x22222222u : 0x11111111u;
         }
         if (!kVisR1 && !PE_PROBE_NOVIS && k < NV && !(kAblate & 16)) {
           const int xr = lx - 3 + k;
@@ -1117,7 +1164,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
             lo = vw == 0 ? q.x : (vw == 1 ? q.y : q.z);
             hi = vw == 0 ? q.y : (vw == 1 ? q.z : q.w);
           }
-          lvis[k * EPB + le] = vo ? ((lo >> vo) | (hi << (32 - vo))) : lo;
+          lvis[k * LS + le] = vo ? ((lo >> vo) | (hi << (32 - vo))) : lo;
         }
       }
     } else {
@@ -1156,7 +1203,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
             const uint64_t hi = w0 + 1 < g.WPR ? ghi[j] : 0ull;
             v = o ? ((glo[j] >> o) | (hi << (64 - o))) : glo[j];
           }
-          lrow[k * EPB + le] = v;
+          lrow[k * LS + le] = v;
         }
       }
 #pragma unroll
@@ -1169,7 +1216,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
             lo = vlo[j];
             hi = vhi[j];
           }
-          lvis[k * EPB + le] = vo ? ((lo >> vo) | (hi << (32 - vo))) : lo;
+          lvis[k * LS + le] = vo ? ((lo >> vo) | (hi << (32 - vo))) : lo;
         }
       }
     }
@@ -1198,16 +1245,41 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   // -> 9.65 us synchronized, 12.88 -> 12.43 us desynchronized; for the whole kernel
   // it slowed the synchronized step)
   if (wv == CW) __builtin_amdgcn_s_setprio(2);
+  // Early record (f32-tile kernels): a block whose ONLY env to truncate this step is
+  // known from its step count (:177; ~6 % of the blocks of a desynchronized batch
+  // each step) has the commit wave load that env's prefetched record and its grid
+  // rows (the terminal info) now, behind the compute phase, so its auto-reset makes
+  // no memory round trip of its own (quad_done_path).  (The byte-coded kernel stages
+  // the same record by LDS-DMA during round 2.)  The loads' only consumer is that
+  // cold path: no wait lands on the hot path.
+  constexpr int KDQ = (5 * C + 27 + 63) / 64, MAXWQ = ONEWORD ? 1 : kCoopWPR;
+  constexpr bool kEarlyRec = !BT && KDQ <= 2;
+  PfLoad<MAXWQ, KDQ> epl;
+  Row4<MAXWQ> eir;
+  int64_t e_early = -1;
+  if constexpr (kEarlyRec) {
+    if (wv == CW && a.pf.scal && a.autoreset && !st.cur) {
+      const uint64_t pmk = __ballot(live && s.step + 1 >= rl.max_steps);
+      const uint32_t plo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pmk),
+                     phi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pmk >> 32));
+      const uint64_t pmu = (uint64_t)plo | ((uint64_t)phi << 32);
+      if (__popcll(pmu) == 1) {
+        e_early = e0 + (__ffsll((unsigned long long)pmu) - 1);
+        coop_load_prefetched<MAXWQ, KDQ>(a.pf, g, e_early, epl, lane);
+        eir = coop_info_rows<MAXWQ>(st, g, e_early, lane);
+      }
+    }
+  }
   s.step = s.step < 65535 ? s.step + 1 : 65535;                  // :162
   bool ok = false, watered = false, wet_hyd = false;
   uint32_t n = 0u;
   int dxv = 0;
   double h = 0.0;
   if (mv) {
-    const uint64_t rt = lrow[(R + 1 + dxm) * EPB + lane];
+    const uint64_t rt = lrow[(R + 1 + dxm) * LS + lane];
     ok = inb && ((rt >> (2 * (nyc + R - yb))) & 3u) != OBST;      // :193-195 (plants walkable)
     if (ok) {
-      n = (lvis[(3 + dxm) * EPB + lane] >> (4 * (nyc + 2 - ybv))) & 15u;
+      n = (lvis[(3 + dxm) * LS + lane] >> (4 * (nyc + 2 - ybv))) & 15u;
       h = n == 0u ? rl.r_exploration : rl.r_revisit;              // :197, 204-207
       dxv = dxm;
     } else {
@@ -1216,7 +1288,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
       h = rl.r_invalid;                                           // :211
     }
   } else if (water) {
-    const uint64_t rc = lrow[(R + 1) * EPB + lane];
+    const uint64_t rc = lrow[(R + 1) * LS + lane];
     const int cd = (int)((rc >> (2 * (s.y + R - yb))) & 3u);
     if (cd == THIRSTY) {                                          // fork plantos_env_new.py:237-240
       watered = true;
@@ -1298,7 +1370,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
           // the window of row nx in LDS (padded nibbles ybv..ybv+7 hold both of its
           // nibbles): one byte store, no read of the word from memory
           const int p = ny + 2, b = p >> 1;
-          const uint32_t wnew = (lvis[(3 + dxm) * EPB + lane] & ~(0xFu << (4 * (p - ybv)))) | (nib << (4 * (p - ybv)));
+          const uint32_t wnew = (lvis[(3 + dxm) * LS + lane] & ~(0xFu << (4 * (p - ybv)))) | (nib << (4 * (p - ybv)));
           st_wt(reinterpret_cast<uint8_t*>(st.vis + e * g.vstride + (int64_t)nx * g.NW) + b,
                 (uint8_t)(wnew >> (4 * (2 * b - ybv))));
           visit_bump_exact(st, g, e, cell_n, n);
@@ -1312,12 +1384,12 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
         if (watered) {
           const int bit = 2 * (s.y + R);
           if constexpr (ONEWORD) {
-            st_wt(const_cast<uint64_t*>(gb) + ox, (uint64_t)(lrow[(R + 1) * EPB + lane] & ~(1ull << bit)));  // code 3 -> 2
+            st_wt(const_cast<uint64_t*>(gb) + ox, (uint64_t)(lrow[(R + 1) * LS + lane] & ~(1ull << bit)));  // code 3 -> 2
           } else {
             // the byte holding the cell's code (padded column c; its 4 cells lie in the
             // window of row x, padded columns yb..yb+31, for R >= 2)
             const int c = s.y + R, B = c >> 2;
-            const uint64_t wr = lrow[(R + 1) * EPB + lane] & ~(1ull << (2 * (c - yb)));  // code 3 -> 2
+            const uint64_t wr = lrow[(R + 1) * LS + lane] & ~(1ull << (2 * (c - yb)));  // code 3 -> 2
             st_wt(reinterpret_cast<uint8_t*>(const_cast<uint64_t*>(gb) + (int64_t)ox * g.WPR) + B,
                   (uint8_t)(wr >> (2 * (4 * B - yb))));
           }
@@ -1360,14 +1432,14 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   const int ndone = __popcll(dmu);
   PE_STAMP(5);
   // auto-reset slow path, out of line (its registers stay off the hot path)
-  static_assert(2 * C * R <= (NR * 8 + NV * 4) * EPB, "LIDAR offset tables must fit the window region");
-  static_assert(5 * 4 * EPB + 8 <= (NR * 8 + NV * 4) * EPB, "reset staging must fit the window region");
+  static_assert(2 * C * R <= (NR * 8 + NV * 4) * LS, "LIDAR offset tables must fit the window region");
+  static_assert(5 * 4 * LS + 8 <= (NR * 8 + NV * 4) * LS, "reset staging must fit the window region");
   const int64_t valid = a.n - e0 < EPB ? a.n - e0 : EPB;
   if (__builtin_expect(any_done, 0)) {  // cold: laid out after the hot path
     const bool staged = stage_ok && npred == 1 && ndone == 1;  // then the done env is the predicted one
     const uint4 ns = quad_done_path<NW, ONEWORD, (5 * C + 27 + 63) / 64, BT>(
         kernargs(), quad_tile_off<R>(), C, R, lane, wv, CW, e0, done, pack(s), ret, ndone, wfix, ctab,
-        staged ? stage : nullptr, staged && stage_info);
+        staged ? stage : nullptr, staged && stage_info, e_early, &epl, &eir);
     s = unpack(ns);
   }
   // the obs tile goes out through the waves other than the commit wave: its state
@@ -2241,6 +2313,11 @@ size_t lds_bytes(const Geo& g) {
 // are the default for the specialized geometries (compile-time C, R: the LIDAR
 // offsets of lidar_tables.inc); the one-lane-per-env kernels stay selectable
 // (PE_STEP_KERNEL=lane, debug builds) for A/B measurement at C16R6 / C64R6.
+// batch sizes up to which the headline kernel runs 16- / 32-env workgroups (quad_epb)
+// (same-box A/B, profiles/r3b_ab_epb*.jsonl: 4096 envs 5.06 -> 4.55 us with 16-env
+// workgroups, 8192: 16 ~ 32, 16384: 32 best, 32768: 32 ~ 64)
+constexpr int kSmallBatch16 = 8192, kSmallBatch32 = 32768;
+
 enum Variant {
   V_GENERIC = 0, V_C16R6_1W = 1, V_C16R6 = 2, V_C64R6 = 3,
   V_QUAD_C16R6_1W = 4, V_QUAD_C16R6 = 5, V_QUAD_C64R6 = 6,
@@ -2264,8 +2341,8 @@ bool is_quad(int v) { return v >= V_QUAD_C16R6_1W; }
 
 int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
   if (is_quad(h->variant)) {
-    const int nw = h->quad_waves;
-    dim3 grid((unsigned)((h->n + kQuadEnvs - 1) / kQuadEnvs)), block(nw * 64);
+    const int nw = h->quad_waves, epb = h->quad_epb;
+    dim3 grid((unsigned)((h->n + epb - 1) / epb)), block(nw * 64);
     size_t lds = quad_lds_bytes(h->g, h->tile_codes);
     if (h->lds_floor > lds) lds = h->lds_floor;  // diagnostics: caps workgroups per CU
 #define PE_QUAD(CC, RR, OW)                                                                 \
@@ -2277,7 +2354,14 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((pe_step_quad<CC, RR, OW, 4>), grid, block, lds, s, a);
 #define PE_QUAD4(CC, RR, OW) hipLaunchKernelGGL((pe_step_quad<CC, RR, OW, 4>), grid, block, lds, s, a);
     switch (h->variant) {
-      case V_QUAD_C16R6_1W: PE_QUAD(16, 6, true); break;
+      case V_QUAD_C16R6_1W:
+        if (epb == 16 && !h->tile_codes)
+          hipLaunchKernelGGL((pe_step_quad<16, 6, true, 4, false, 16>), grid, block, lds, s, a);
+        else if (epb == 32 && !h->tile_codes)
+          hipLaunchKernelGGL((pe_step_quad<16, 6, true, 4, false, 32>), grid, block, lds, s, a);
+        else
+          PE_QUAD(16, 6, true);
+        break;
       case V_QUAD_C16R6: PE_QUAD4(16, 6, false); break;
       case V_QUAD_C64R6: PE_QUAD(64, 6, false); break;
       case V_QUAD_C10R2_1W: PE_QUAD4(10, 2, true); break;
@@ -2602,7 +2686,25 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
     if (std::strcmp(kenv, "wave") == 0) h->variant = V_GENERIC;  // A/B: the one-wave-per-env kernel
 #endif
   if (!is_quad(h->variant)) h->tile_codes = 0;
+  // envs per workgroup: a batch too small to give every CU four 64-env workgroups
+  // (1024 at 65536 envs) is cut into 16- or 32-env workgroups instead, so that it
+  // still spreads over all 256 CUs (headline geometry's kernel only; 4 waves, f32 tile)
+  h->quad_epb = kQuadEnvs;
+  if (h->variant == V_QUAD_C16R6_1W && !h->tile_codes && h->quad_waves == 4)
+    h->quad_epb = n_envs <= kSmallBatch16 ? 16 : (n_envs <= kSmallBatch32 ? 32 : kQuadEnvs);
+#ifdef PE_DEBUG_KNOBS
+  if (const char* ep = std::getenv("PE_QUAD_EPB"))
+    if (h->variant == V_QUAD_C16R6_1W && !h->tile_codes && h->quad_waves == 4) {
+      const int v = std::atoi(ep);
+      h->quad_epb = v == 16 || v == 32 ? v : kQuadEnvs;
+    }
+#endif
   h->kname = variant_name(h->variant);
+  if (h->quad_epb != kQuadEnvs) {
+    std::snprintf(h->kname_buf, sizeof(h->kname_buf), "%.*s,E%d>", (int)std::strlen(h->kname) - 1, h->kname,
+                  h->quad_epb);
+    h->kname = h->kname_buf;
+  }
   // explicit reset-path tuning (pe_config.coop_max_done; -1: the choice above) --
   // applied before the prefetch decision, which depends on it
   if (c->coop_max_done >= 0 && coop_reset_ok(G, R, g.WPR, g.NW, P, C, c->map_generation_algo))

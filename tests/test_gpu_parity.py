@@ -153,7 +153,18 @@ def test_device_reset_matches_oracle_philox(name):
 @pytest.mark.parametrize("name", sorted(KERNELS))
 def test_kernel_selection(name):
     b = make(CFG[name], 64)
-    assert b.kernel_name == KERNELS[name]
+    # the headline geometry's small batches run 16-env workgroups (see below)
+    assert b.kernel_name == (KERNELS[name][:-1] + ",E16>" if name == "g20" else KERNELS[name])
+    b.close()
+
+
+@pytest.mark.parametrize("n,suffix", [(1, ",E16"), (4096, ",E16"), (8192, ",E16"), (8193, ",E32"),
+                                      (32768, ",E32"), (32769, ""), (65536, "")])
+def test_small_batch_workgroup_shape(n, suffix):
+    """Batches too small for four 64-env workgroups per CU run 16- or 32-env
+    workgroups of the same kernel (pe_create's choice, by batch size)"""
+    b = make(CFG["g20"], n)
+    assert b.kernel_name == "pe_step_quad<C16,R6,1word" + suffix + ">"
     b.close()
 
 
@@ -192,9 +203,12 @@ def test_rollout_parity_device_rng(name, n, steps):
     b.close()
 
 
-@pytest.mark.parametrize("name,desync", [("g20", False), ("g20", True), ("g64", False), ("g64", True),
-                                         ("g64r32", True), ("g25", False), ("g25", True)])
-def test_full_batch_sampled_parity_and_invariants(name, desync):
+@pytest.mark.parametrize("name,desync,n", [("g20", False, 65536), ("g20", True, 65536), ("g64", False, 65536),
+                                           ("g64", True, 65536), ("g64r32", True, 65536), ("g25", False, 65536),
+                                           ("g25", True, 65536),
+                                           # BASELINE config 2 (16-env workgroups) and a 32-env-workgroup batch
+                                           ("g20", False, 4096), ("g20", True, 4096), ("g20", True, 20000)])
+def test_full_batch_sampled_parity_and_invariants(name, desync, n):
     """65536 envs (BASELINE headline 20x20/16 rays, the 64x64/64-ray stress config,
     and 25x25/16 rays -- the geometry the reference's training scripts build,
     A2C_training.py:206-212, trainingCode.py:121-125) for 1010+ steps, crossing the 1000-step truncation: the oracle replays
@@ -206,9 +220,9 @@ def test_full_batch_sampled_parity_and_invariants(name, desync):
     cooperative reset paths."""
     cfg = CFG[name]
     G, C, R = cfg[0], cfg[4], cfg[3]
-    n, seed, steps = 65536, 5, 1010 if name.startswith("g64") else 1100
+    seed, steps = 5, 1010 if name.startswith("g64") else 1100
     b = make(cfg, n, seed=seed)
-    sample = np.r_[0:64, 30000:30064, 65472:65536]
+    sample = np.unique(np.r_[0:64, n // 2 - 32:n // 2 + 32, n - 64:n])
     ov = OracleVec(cfg, sample, seed)
     start = np.zeros(n, np.int32)
     if desync:
