@@ -897,7 +897,7 @@ __device__ __forceinline__ void quad_done_obs(const void* ka, int tile_off, int 
 // a batch of a few thousand envs spreads over every CU -- lanes >= EPB idle).  The
 // LDS layout keeps the 64-env stride LS whatever EPB.
 template <int C, int R, bool ONEWORD, int NW, bool BT = false, int EPB = kQuadEnvs>
-__global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs; NW=4: <= 128 VGPRs (4 workgroups per CU: G=25 13.1 -> 10.5 us; 1-word C16: 122 -> 104 VGPRs)
+__global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs (small-batch EPB: one workgroup per CU, no cap); NW=4: <= 128 VGPRs (4 workgroups per CU: G=25 13.1 -> 10.5 us; 1-word C16: 122 -> 104 VGPRs)
   constexpr int NR = 2 * R + 3, NV = 7, LS = kQuadEnvs, CW = NW - 1;  // CW: commit wave
   static_assert(EPB == 16 || EPB == 32 || EPB == 64, "envs per workgroup");
   static_assert(!BT || EPB == kQuadEnvs, "the byte-coded kernel's LDS-DMA staging predicts over all 64 lanes");
@@ -1174,13 +1174,25 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
       constexpr int JG = (NR + LT - 1) / LT, JV = (NV + LT - 1) / LT;
       uint64_t glo[JG], ghi[JG];
       uint32_t vlo[JV], vhi[JV];
+      if (g.WPR == 2) {  // (G <= 52, e.g. the training scripts' 25x25) a row is one aligned 16-B load
 #pragma unroll
-      for (int j = 0; j < JG; ++j) {
-        const int xr = base + sub + LT * j;
-        const int xc = xr < 0 ? 0 : (xr >= g.G ? g.G - 1 : xr);
-        const uint64_t* p = lgb + (int64_t)xc * g.WPR;
-        glo[j] = p[w0];
-        ghi[j] = p[w1];
+        for (int j = 0; j < JG; ++j) {
+          const int xr = base + sub + LT * j;
+          const int xc = xr < 0 ? 0 : (xr >= g.G ? g.G - 1 : xr);
+          const uint4 q = *reinterpret_cast<const uint4*>(lgb + (int64_t)xc * 2);
+          const uint64_t lo64 = (uint64_t)q.x | ((uint64_t)q.y << 32), hi64 = (uint64_t)q.z | ((uint64_t)q.w << 32);
+          glo[j] = w0 ? hi64 : lo64;
+          ghi[j] = hi64;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < JG; ++j) {
+          const int xr = base + sub + LT * j;
+          const int xc = xr < 0 ? 0 : (xr >= g.G ? g.G - 1 : xr);
+          const uint64_t* p = lgb + (int64_t)xc * g.WPR;
+          glo[j] = p[w0];
+          ghi[j] = p[w1];
+        }
       }
       const int lybv = ly > 0 ? ly - 1 : 0;
       const int vw = (4 * lybv) >> 5, vo = (4 * lybv) & 31;
@@ -1245,7 +1257,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   // -> 9.65 us synchronized, 12.88 -> 12.43 us desynchronized; for the whole kernel
   // it slowed the synchronized step)
   if (wv == CW) __builtin_amdgcn_s_setprio(2);
-  // Early record (f32-tile kernels): a block whose ONLY env to truncate this step is
+  // Early record (f32-tile one-word kernels): a block whose ONLY env to truncate this step is
   // known from its step count (:177; ~6 % of the blocks of a desynchronized batch
   // each step) has the commit wave load that env's prefetched record and its grid
   // rows (the terminal info) now, behind the compute phase, so its auto-reset makes
@@ -1253,7 +1265,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 8 : 4) void pe_step_quad(StepArg
   // the same record by LDS-DMA during round 2.)  The loads' only consumer is that
   // cold path: no wait lands on the hot path.
   constexpr int KDQ = (5 * C + 27 + 63) / 64, MAXWQ = ONEWORD ? 1 : kCoopWPR;
-  constexpr bool kEarlyRec = !BT && KDQ <= 2;
+  // (one-word 64-env kernels only: the multi-word kernel is at its 128-VGPR cap and
+  // spilled with it -- 25x25 desynchronized 14.0 -> 14.6 us -- and the 16-env shape of
+  // small batches lost 2-5 % synchronized; profiles/r3c_ab_early_*.jsonl)
+  constexpr bool kEarlyRec = !BT && ONEWORD && EPB == LS && KDQ <= 2;
   PfLoad<MAXWQ, KDQ> epl;
   Row4<MAXWQ> eir;
   int64_t e_early = -1;
@@ -2355,7 +2370,9 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
 #define PE_QUAD4(CC, RR, OW) hipLaunchKernelGGL((pe_step_quad<CC, RR, OW, 4>), grid, block, lds, s, a);
     switch (h->variant) {
       case V_QUAD_C16R6_1W:
-        if (epb == 16 && !h->tile_codes)
+        if (epb == 16 && !h->tile_codes && nw == 8)
+          hipLaunchKernelGGL((pe_step_quad<16, 6, true, 8, false, 16>), grid, block, lds, s, a);
+        else if (epb == 16 && !h->tile_codes)
           hipLaunchKernelGGL((pe_step_quad<16, 6, true, 4, false, 16>), grid, block, lds, s, a);
         else if (epb == 32 && !h->tile_codes)
           hipLaunchKernelGGL((pe_step_quad<16, 6, true, 4, false, 32>), grid, block, lds, s, a);
@@ -2694,9 +2711,9 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
     h->quad_epb = n_envs <= kSmallBatch16 ? 16 : (n_envs <= kSmallBatch32 ? 32 : kQuadEnvs);
 #ifdef PE_DEBUG_KNOBS
   if (const char* ep = std::getenv("PE_QUAD_EPB"))
-    if (h->variant == V_QUAD_C16R6_1W && !h->tile_codes && h->quad_waves == 4) {
+    if (h->variant == V_QUAD_C16R6_1W && !h->tile_codes) {
       const int v = std::atoi(ep);
-      h->quad_epb = v == 16 || v == 32 ? v : kQuadEnvs;
+      h->quad_epb = v == 16 || (v == 32 && h->quad_waves == 4) ? v : kQuadEnvs;  // 8 waves: 16 or 64
     }
 #endif
   h->kname = variant_name(h->variant);

@@ -230,7 +230,7 @@ class PlantOSVecEnv(_VecEnvBase):
     def __init__(self, num_envs, grid_size=21, num_plants=8, num_obstacles=50, lidar_range=2, lidar_channels=10,
                  thirsty_plant_prob=0.7, max_steps=1000, seed=0, device=None, tensors=False, env_id_offset=0,
                  observation_mode="lidar", render_mode=None, batch=None, reset_mode="device", python_seed=None,
-                 curriculum=False, map_generation_algo="original", host_buffers=0):
+                 curriculum=False, map_generation_algo="original", host_buffers=0, prefetch_every=None):
         """reset_mode="device": maps from the device generator keyed by (seed, env id,
         episode) -- the throughput mode.  reset_mode="cpython": the reference's own
         layouts, seed-exact: CPython's global `random` after random.seed(python_seed)
@@ -247,7 +247,9 @@ class PlantOSVecEnv(_VecEnvBase):
         host_buffers=k (numpy face): obs arrive in a ring of k pinned host buffers
         (one DMA at full PCIe rate; each returned obs array stays valid for k steps,
         enough for SB3's collect_rollouts with k >= 2); 0 (default): a fresh array
-        per step, as DummyVecEnv returns."""
+        per step, as DummyVecEnv returns.
+        prefetch_every: pe_config.prefetch_every (steps between the launches that
+        generate next-episode maps ahead of time; None: the library's 256, 0: off)."""
         if observation_mode != "lidar":
             raise ValueError("only observation_mode='lidar' exists in the reference (plantos_env.py:27)")
         if reset_mode not in ("device", "cpython"):
@@ -257,7 +259,7 @@ class PlantOSVecEnv(_VecEnvBase):
             num_envs, grid_size=grid_size, num_plants=num_plants, num_obstacles=num_obstacles,
             lidar_range=lidar_range, lidar_channels=lidar_channels, thirsty_plant_prob=thirsty_plant_prob,
             max_steps=max_steps, autoreset=reset_mode == "device", seed=seed, env_id_offset=env_id_offset,
-            device=device, map_generation_algo=map_generation_algo)
+            device=device, map_generation_algo=map_generation_algo, prefetch_every=prefetch_every)
         if curriculum:
             # True / "a2c": A2C_training.py:37-109 as :121 builds it; "trainingCode":
             # trainingCode.py:24-98 as :107 builds it; a dict: {"variant": ..., overrides}
