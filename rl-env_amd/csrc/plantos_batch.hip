@@ -661,17 +661,20 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         float tv[KD];
 #pragma unroll
         for (int j = 0; j < KD; ++j) tv[j] = lane + 64 * j < g.D ? tval(orow, lane + 64 * j) : 0.0f;
+        PE_DSTAMP(1);
         if (a.tinfo) coop_info_store<MAXW>(st, g, *early_rows, sv, a.tinfo + el * PE_NINFO, lane, wf, ltab);
+        PE_DSTAMP(2);
         Row4<MAXW> rw;
         Scal ns;
         asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
         if (take(el, sv.episode, *early, rw, ns, orow)) {
-          ns = coop_apply_reset<MAXW>(st, g, el, ns, false, rw, lane);
+          ns = coop_apply_reset<MAXW>(st, g, el, ns, false, rw, lane, ltab);
         } else {  // the record is not this reset's (not generated yet): generate in place
           uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
-          ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, false, rw, lane, scr);
+          ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, false, rw, lane, scr, ltab);
           coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
         }
+        PE_DSTAMP(3);
         if (a.tobs) {
           float* t = a.tobs + el * g.D;
 #pragma unroll
@@ -679,11 +682,13 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
             if (lane + 64 * j < g.D) t[lane + 64 * j] = tv[j];
         }
         if (lane == 0) a.pf.flag[el] = 1;  // its next map goes into the next generating batch
+        PE_DSTAMP(4);
         if (done) {  // lane l: program order after its commit stores
           s = ns;
           st.ep_ret[e] = 0.0;
           st.scal[e] = pack(s);
         }
+        PE_DSTAMP(5);
       } else {
         // the record: staged into LDS before the done barrier (stage), or loaded now
         PfLoad<MAXW, KD> pl;
@@ -712,7 +717,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
                                                       g, lane),
                                   sv, a.tinfo + el * PE_NINFO, lane, wf, ltab);
           else
-            coop_write_info<MAXW>(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, wf);
+            coop_write_info<MAXW>(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, wf, ltab);
         }
         PE_DSTAMP(2);
         Row4<MAXW> rw;
@@ -721,10 +726,10 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         const bool took = stage ? pf_stage_take<MAXW>(stage, g, (int)a.pf.ostride, sv.episode, rw, ns, orow, lane)
                                 : (a.pf.scal && take(el, sv.episode, pl, rw, ns, orow));
         if (took) {
-          ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane);
+          ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane, ltab);
         } else {
           uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
-          ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane, scr);
+          ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane, scr, ltab);
           coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
         }
         PE_DSTAMP(3);
@@ -796,15 +801,15 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         // the prefetched record's loads go out first, the terminal info's after them
         PfLoad<MAXW, KD> pl;
         if (a.pf.scal) coop_load_prefetched<MAXW, KD>(a.pf, g, el, pl, lane);
-        if (a.tinfo) coop_write_info<MAXW>(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, kw >> 1);
+        if (a.tinfo) coop_write_info<MAXW>(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, kw >> 1, ltab);
         Row4<MAXW> rw;
         Scal ns;
         asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
         if (a.pf.scal && take(el, sv.episode, pl, rw, ns, orow)) {
-          ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane);
+          ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane, ltab);
         } else {
           uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
-          ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane, scr);
+          ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane, scr, ltab);
           coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
         }
         if (a.pf.scal && lane == 0) a.pf.flag[el] = 1;  // its next map goes into the next generating batch
@@ -1053,6 +1058,36 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   const uint64_t* gb = st.grid + e * g.gstride;
   const int cell_o = s.x * g.G + s.y, cell_n = nx * g.G + nyc;
 
+  // Early record (f32-tile one-word kernels): a block whose ONLY env to truncate this
+  // step is known from its step count (:177; ~6 % of the blocks of a desynchronized
+  // batch each step) has the commit wave load that env's prefetched record and its
+  // grid rows (the terminal info) right before round 2's loads -- they land with them,
+  // and the barrier after round 2 has waited for them -- so its auto-reset makes no
+  // memory round trip of its own (quad_done_path).  Issued behind the compute phase
+  // instead, the done path's first use waited for the commit's stores too (vmcnt
+  // counts both, in order).  (The byte-coded kernel stages the same record by
+  // LDS-DMA during round 2.)
+  constexpr int KDQ = (5 * C + 27 + 63) / 64, MAXWQ = ONEWORD ? 1 : kCoopWPR;
+  // (one-word 64-env kernels only: the multi-word kernel is at its 128-VGPR cap and
+  // spilled with it -- 25x25 desynchronized 14.0 -> 14.6 us -- and the 16-env shape of
+  // small batches lost 2-5 % synchronized; profiles/r3c_ab_early_*.jsonl)
+  constexpr bool kEarlyRec = !BT && ONEWORD && EPB == LS && KDQ <= 2;
+  PfLoad<MAXWQ, KDQ> epl;
+  Row4<MAXWQ> eir;
+  int64_t e_early = -1;
+  if constexpr (kEarlyRec) {
+    if (wv == CW && a.pf.scal && a.autoreset && !st.cur) {
+      const uint64_t pmk = __ballot(live && s.step + 1 >= rl.max_steps);
+      const uint32_t plo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pmk),
+                     phi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pmk >> 32));
+      const uint64_t pmu = (uint64_t)plo | ((uint64_t)phi << 32);
+      if (__popcll(pmu) == 1) {
+        e_early = e0 + (__ffsll((unsigned long long)pmu) - 1);
+        coop_load_prefetched<MAXWQ, KDQ>(a.pf, g, e_early, epl, lane);
+        eir = coop_info_rows<MAXWQ>(st, g, e_early, lane);
+      }
+    }
+  }
   // ---- round 2: window rows of env le -> LDS [row][env] (loader role)
   uint32_t eo = 0u, en = 0u;
   if (llive && !(kAblate & 4)) {
@@ -1257,34 +1292,6 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // -> 9.65 us synchronized, 12.88 -> 12.43 us desynchronized; for the whole kernel
   // it slowed the synchronized step)
   if (wv == CW) __builtin_amdgcn_s_setprio(2);
-  // Early record (f32-tile one-word kernels): a block whose ONLY env to truncate this step is
-  // known from its step count (:177; ~6 % of the blocks of a desynchronized batch
-  // each step) has the commit wave load that env's prefetched record and its grid
-  // rows (the terminal info) now, behind the compute phase, so its auto-reset makes
-  // no memory round trip of its own (quad_done_path).  (The byte-coded kernel stages
-  // the same record by LDS-DMA during round 2.)  The loads' only consumer is that
-  // cold path: no wait lands on the hot path.
-  constexpr int KDQ = (5 * C + 27 + 63) / 64, MAXWQ = ONEWORD ? 1 : kCoopWPR;
-  // (one-word 64-env kernels only: the multi-word kernel is at its 128-VGPR cap and
-  // spilled with it -- 25x25 desynchronized 14.0 -> 14.6 us -- and the 16-env shape of
-  // small batches lost 2-5 % synchronized; profiles/r3c_ab_early_*.jsonl)
-  constexpr bool kEarlyRec = !BT && ONEWORD && EPB == LS && KDQ <= 2;
-  PfLoad<MAXWQ, KDQ> epl;
-  Row4<MAXWQ> eir;
-  int64_t e_early = -1;
-  if constexpr (kEarlyRec) {
-    if (wv == CW && a.pf.scal && a.autoreset && !st.cur) {
-      const uint64_t pmk = __ballot(live && s.step + 1 >= rl.max_steps);
-      const uint32_t plo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pmk),
-                     phi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pmk >> 32));
-      const uint64_t pmu = (uint64_t)plo | ((uint64_t)phi << 32);
-      if (__popcll(pmu) == 1) {
-        e_early = e0 + (__ffsll((unsigned long long)pmu) - 1);
-        coop_load_prefetched<MAXWQ, KDQ>(a.pf, g, e_early, epl, lane);
-        eir = coop_info_rows<MAXWQ>(st, g, e_early, lane);
-      }
-    }
-  }
   s.step = s.step < 65535 ? s.step + 1 : 65535;                  // :162
   bool ok = false, watered = false, wet_hyd = false;
   uint32_t n = 0u;
@@ -2331,7 +2338,7 @@ size_t lds_bytes(const Geo& g) {
 // batch sizes up to which the headline kernel runs 16- / 32-env workgroups (quad_epb)
 // (same-box A/B, profiles/r3b_ab_epb*.jsonl: 4096 envs 5.06 -> 4.55 us with 16-env
 // workgroups, 8192: 16 ~ 32, 16384: 32 best, 32768: 32 ~ 64)
-constexpr int kSmallBatch16 = 8192, kSmallBatch32 = 32768;
+constexpr int kSmallBatch16 = 8192, kSmallBatch32 = 32768, kSmallBatch8W = 4096;
 
 enum Variant {
   V_GENERIC = 0, V_C16R6_1W = 1, V_C16R6 = 2, V_C64R6 = 3,
@@ -2706,9 +2713,13 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   // envs per workgroup: a batch too small to give every CU four 64-env workgroups
   // (1024 at 65536 envs) is cut into 16- or 32-env workgroups instead, so that it
   // still spreads over all 256 CUs (headline geometry's kernel only; 4 waves, f32 tile)
+  // (up to 4096 envs: 8 waves x 16 envs -- two waves per SIMD on every CU, sectors of 2
+  // rays: 2048 envs 4.56 -> 4.41 us, 4096 4.56 -> 4.49; 8192 4.82 -> 4.98 us, kept at 4)
   h->quad_epb = kQuadEnvs;
-  if (h->variant == V_QUAD_C16R6_1W && !h->tile_codes && h->quad_waves == 4)
+  if (h->variant == V_QUAD_C16R6_1W && !h->tile_codes && h->quad_waves == 4) {
     h->quad_epb = n_envs <= kSmallBatch16 ? 16 : (n_envs <= kSmallBatch32 ? 32 : kQuadEnvs);
+    if (n_envs <= kSmallBatch8W) h->quad_waves = 8;
+  }
 #ifdef PE_DEBUG_KNOBS
   if (const char* ep = std::getenv("PE_QUAD_EPB"))
     if (h->variant == V_QUAD_C16R6_1W && !h->tile_codes) {
@@ -2718,8 +2729,8 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
 #endif
   h->kname = variant_name(h->variant);
   if (h->quad_epb != kQuadEnvs) {
-    std::snprintf(h->kname_buf, sizeof(h->kname_buf), "%.*s,E%d>", (int)std::strlen(h->kname) - 1, h->kname,
-                  h->quad_epb);
+    std::snprintf(h->kname_buf, sizeof(h->kname_buf), "%.*s%s,E%d>", (int)std::strlen(h->kname) - 1, h->kname,
+                  h->quad_waves == 8 ? ",W8" : "", h->quad_epb);
     h->kname = h->kname_buf;
   }
   // explicit reset-path tuning (pe_config.coop_max_done; -1: the choice above) --

@@ -154,15 +154,16 @@ def test_device_reset_matches_oracle_philox(name):
 def test_kernel_selection(name):
     b = make(CFG[name], 64)
     # the headline geometry's small batches run 16-env workgroups (see below)
-    assert b.kernel_name == (KERNELS[name][:-1] + ",E16>" if name == "g20" else KERNELS[name])
+    assert b.kernel_name == (KERNELS[name][:-1] + ",W8,E16>" if name == "g20" else KERNELS[name])
     b.close()
 
 
-@pytest.mark.parametrize("n,suffix", [(1, ",E16"), (4096, ",E16"), (8192, ",E16"), (8193, ",E32"),
-                                      (32768, ",E32"), (32769, ""), (65536, "")])
+@pytest.mark.parametrize("n,suffix", [(1, ",W8,E16"), (4096, ",W8,E16"), (4097, ",E16"), (8192, ",E16"),
+                                      (8193, ",E32"), (32768, ",E32"), (32769, ""), (65536, "")])
 def test_small_batch_workgroup_shape(n, suffix):
     """Batches too small for four 64-env workgroups per CU run 16- or 32-env
-    workgroups of the same kernel (pe_create's choice, by batch size)"""
+    workgroups of the same kernel, up to 4096 envs with 8 waves (sectors of 2 rays)
+    -- pe_create's choice, by batch size"""
     b = make(CFG["g20"], n)
     assert b.kernel_name == "pe_step_quad<C16,R6,1word" + suffix + ">"
     b.close()
