@@ -175,6 +175,23 @@ def measured_traffic(cfg, sha):
 
 
 # ---------------------------------------------------------------- timed windows
+def upload_graph(torch, gr):
+    """hipGraphUpload the captured graph before the timed window (executes nothing):
+    its first replay otherwise pays the upload, ~1 us per step of a 20-step window
+    (profiles/r3g_window_first_replay.json).  Best effort: a runtime without it
+    just uploads at the first replay."""
+    import ctypes
+    import glob
+    try:
+        lib = glob.glob(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so*"))
+        hip = ctypes.CDLL(lib[0] if lib else "libamdhip64.so")
+        exe = gr.raw_cuda_graph_exec()
+        hip.hipGraphUpload.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        return hip.hipGraphUpload(ctypes.c_void_p(exe), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
+    except (OSError, AttributeError, IndexError, RuntimeError):
+        return False
+
+
 def plan_graph(K, graph_max, pf):
     """Steps per captured graph for a K-step window (0: direct launches).  A window of
     K <= graph_max steps is one K-step graph replayed once; a longer one replays a
@@ -401,18 +418,22 @@ def main():
         with torch.cuda.graph(gr):
             for k in range(steps):
                 b.step(actions[k % T])
+        upload_graph(torch, gr)
         torch.cuda.synchronize()
         return gr
 
-    for t in range(args.warmup):
-        one_step(t)
-    torch.cuda.synchronize()
     K = args.steps
     # graph mode: one graph = `chunk` consecutive pe_step launches; step k of a replay
     # reads action row k % T (plain mode: step t reads row t % T).  K = reps * chunk + rest.
+    # Captured (nothing executes) BEFORE the warm-up, so that the warm-up steps run
+    # right up to the timed window: a GPU left idle while the host captures starts the
+    # window below its clocks (driver-shaped 20-step windows: ~1 us per step)
     pf = b.prefetch_every
     chunk = plan_graph(K, args.graph, pf)
     graph = capture(chunk)
+    for t in range(args.warmup):
+        one_step(t)
+    torch.cuda.synchronize()
     elapsed, kern_ms = timed(torch, dist, device, K, one_step, chunk, graph)
     b.raise_on_errors()
     total_steps = n * K * world
@@ -424,11 +445,11 @@ def main():
     if args.desync_steps > 0 and not args.desync:
         desynchronize(torch, b, args.seed)
         Kd = args.desync_steps
+        d_chunk = plan_graph(Kd, args.graph, pf)
+        d_graph = graph if d_chunk == chunk else capture(d_chunk)
         for t in range(200):
             one_step(t)
         torch.cuda.synchronize()
-        d_chunk = plan_graph(Kd, args.graph, pf)
-        d_graph = graph if d_chunk == chunk else capture(d_chunk)
         d_el, d_kms = timed(torch, dist, device, Kd, one_step, d_chunk, d_graph)
         d_ach = B * n / (d_kms * 1e-3) / 1e9
         desync = {"value": n * Kd * world / d_el, "unit": "env-steps/s", "steps": Kd,

@@ -798,14 +798,21 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         const int kw = __builtin_amdgcn_readfirstlane((int)stage[5 * l + 4]);
         const bool kp = (kw & 1) != 0;
         const Scal sv = unpack(sl);
-        // the prefetched record's loads go out first, the terminal info's after them
+        // the prefetched record's loads go out first, the terminal info's after them --
+        // or both came with round 2 (the kernel's early record of this wave's env)
+        const bool eh = !BT && KD <= 2 && early != nullptr && el == e_early;
         PfLoad<MAXW, KD> pl;
-        if (a.pf.scal) coop_load_prefetched<MAXW, KD>(a.pf, g, el, pl, lane);
-        if (a.tinfo) coop_write_info<MAXW>(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, kw >> 1, ltab);
+        if (a.pf.scal && !eh) coop_load_prefetched<MAXW, KD>(a.pf, g, el, pl, lane);
+        if (a.tinfo) {
+          if (eh)
+            coop_info_store<MAXW>(st, g, *early_rows, sv, a.tinfo + el * PE_NINFO, lane, kw >> 1, ltab);
+          else
+            coop_write_info<MAXW>(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, kw >> 1, ltab);
+        }
         Row4<MAXW> rw;
         Scal ns;
         asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
-        if (a.pf.scal && take(el, sv.episode, pl, rw, ns, orow)) {
+        if (a.pf.scal && take(el, sv.episode, eh ? *early : pl, rw, ns, orow)) {
           ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane, ltab);
         } else {
           uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
@@ -954,7 +961,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // one-word rows (G <= 20): the loader env's whole grid block (gstride / 2 <= 10
   // 16-B units, contiguous, 3 per loader thread) comes in round 1 -- its address does
   // not depend on the position -- and only the visit rows are left for round 2
-  constexpr int JG1 = (10 + LT - 1) / LT;  // gstride / 2 <= 10 16-B units (G <= 20)
+  // gstride / 2 16-B units: one-word rows need G + 2R <= 32 (C16R6: G <= 20, 10 units)
+  constexpr int JG1 = ((32 - 2 * R + 1) / 2 + LT - 1) / LT;
   constexpr bool kGridR1 = ONEWORD && PE_GRID_R1;
   uint4 qg1[kGridR1 ? JG1 : 1];
   if constexpr (kGridR1) {
@@ -1076,6 +1084,9 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   Row4<MAXWQ> eir;
   int64_t e_early = -1;
   if constexpr (kEarlyRec) {
+    // (the commit wave only, for a block with exactly one: records for up to one
+    // predicted env per wave took the desynchronized step 11.16 -> 11.06 us but the
+    // synchronized one 9.42 -> 9.49, profiles/r3g_ab_*.jsonl)
     if (wv == CW && a.pf.scal && a.autoreset && !st.cur) {
       const uint64_t pmk = __ballot(live && s.step + 1 >= rl.max_steps);
       const uint32_t plo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pmk),
@@ -1231,13 +1242,25 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
       }
       const int lybv = ly > 0 ? ly - 1 : 0;
       const int vw = (4 * lybv) >> 5, vo = (4 * lybv) & 31;
-      const uint32_t* vb = st.vis + el * g.vstride + vw;
+      if (g.NW == 4) {  // (G <= 25) 16-B rows: one load per row, words vw, vw + 1 <= 3 selected
+        const uint4* vq = reinterpret_cast<const uint4*>(st.vis + el * g.vstride);
 #pragma unroll
-      for (int j = 0; j < JV; ++j) {
-        const int xr = lx - 3 + sub + LT * j;
-        const int xc = xr < 0 ? 0 : (xr >= g.G ? g.G - 1 : xr);
-        vlo[j] = vb[(int64_t)xc * g.NW];
-        vhi[j] = vb[(int64_t)xc * g.NW + 1];  // vw + 1 < NW always (one spare word per row)
+        for (int j = 0; j < JV; ++j) {
+          const int xr = lx - 3 + sub + LT * j;
+          const int xc = xr < 0 ? 0 : (xr >= g.G ? g.G - 1 : xr);
+          const uint4 q = vq[xc];
+          vlo[j] = vw == 0 ? q.x : (vw == 1 ? q.y : q.z);
+          vhi[j] = vw == 0 ? q.y : (vw == 1 ? q.z : q.w);
+        }
+      } else {
+        const uint32_t* vb = st.vis + el * g.vstride + vw;
+#pragma unroll
+        for (int j = 0; j < JV; ++j) {
+          const int xr = lx - 3 + sub + LT * j;
+          const int xc = xr < 0 ? 0 : (xr >= g.G ? g.G - 1 : xr);
+          vlo[j] = vb[(int64_t)xc * g.NW];
+          vhi[j] = vb[(int64_t)xc * g.NW + 1];  // vw + 1 < NW always (one spare word per row)
+        }
       }
       stage_issue();
 #pragma unroll
@@ -1282,6 +1305,12 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
 #ifdef PE_STAMPS
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #endif
+  // the commit wave's early record landed with round 2: a wait the compiler tracks
+  // (not asm), so that the done path's first use of it carries none -- otherwise it
+  // waits vmcnt(0) there, i.e. for the commit's stores too (in-order counter)
+  if constexpr (kEarlyRec) {
+    if (wv == CW) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  }
   PE_STAMP(2);
   __syncthreads();
   PE_STAMP(3);
@@ -1292,6 +1321,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // -> 9.65 us synchronized, 12.88 -> 12.43 us desynchronized; for the whole kernel
   // it slowed the synchronized step)
   if (wv == CW) __builtin_amdgcn_s_setprio(2);
+  // (Tried: the early record's state writes issued here, at the start of the compute
+  // phase, instead of in the done path: the commit wave then waited for them before
+  // re-using their data registers -- desynchronized 11.12 -> 12.05 us, synchronized
+  // 9.47 -> 9.59; profiles/r3i_ab_*.jsonl.)
   s.step = s.step < 65535 ? s.step + 1 : 65535;                  // :162
   bool ok = false, watered = false, wet_hyd = false;
   uint32_t n = 0u;
@@ -2582,8 +2615,12 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   g.DS = g.D | 1;
   g.GG = G * G;
   g.WPR = (2 * (G + 2 * R) + 63) / 64;
-  g.NW = (4 * (G + 4) + 31) / 32 + 1;
-  if (g.NW < 4) g.NW = 4;  // 16-B visit rows: one dwordx4 per row in the sector kernel
+  // visit row words: the padded row's G+4 nibbles + a spare word, so that the 8-nibble
+  // window starting at any padded column y-1 (words vw, vw+1) stays inside the row.
+  // Up to G = 25, 4 words already do (vw <= 2): 16-B rows, one dwordx4 per window row
+  // in the sector kernels (the reference's training grid, 25x25, and the constructor
+  // default's 21x21 included)
+  g.NW = G <= 25 ? 4 : (4 * (G + 4) + 31) / 32 + 1;
   g.EW = (g.GG + 31) / 32;
   g.gstride = (int64_t)align_up((size_t)G * g.WPR, 2);  // 16-B aligned env blocks (row-pair loads)
   g.vstride = (int64_t)G * g.NW;
@@ -2681,7 +2718,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   if (!lane_kernels && C == 16 && R == 4 && table_matches<16, 4>(ldx, ldy)) h->variant = V_QUAD_C16R4_1W;
   if (h->variant >= V_QUAD_C10R2_1W) h->quad_waves = 4;
   // the one-word form (whole padded row in one u64) needs WPR == 1 and 16-B visit
-  // rows (NW == 4: G <= 20); otherwise the multi-word (funnel-shifted) form
+  // rows (NW == 4: G <= 25); otherwise the multi-word (funnel-shifted) form
   const bool oneword = g.WPR == 1 && g.NW == 4;
   if ((h->variant == V_QUAD_C10R2_1W || h->variant == V_QUAD_C16R4_1W) && !oneword) h->variant += 1;
   if (h->variant == V_QUAD_C16R6_1W && g.NW != 4) h->variant = V_C16R6_1W;  // needs 16-B visit rows

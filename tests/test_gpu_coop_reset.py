@@ -25,6 +25,7 @@ CFG = {
     "g15": (15, 6, 8, 4, 16),     # one-word C16R4 sector kernel (test_environment.py:24)
     "g12r2": (12, 4, 6, 2, 10),   # one-word C10R2
     "g64r32": (64, 100, 120, 32, 64),  # the one-wave-per-env kernel (long rays)
+    "g30r2": (30, 12, 40, 2, 10),  # multi-word C10R2
 }
 
 
@@ -50,6 +51,7 @@ def info_rows(b, idx):
     ("g25", 600, 80, 60, None, None, None, None, False),
     ("g15", 600, 80, 60, None, None, None, None, False),
     ("g12r2", 600, 80, 60, None, None, None, None, False),
+    ("g30r2", 400, 60, 50, None, None, None, None, False),
     ("g64r32", 192, 50, 40, None, None, None, None, False),
     ("g64r32", 128, 12, 1, "0", None, None, None, False),    # dense: serial resets (coop_max_done 0)
     ("g21", 256, 12, 1, "0", None, None, None, False),        # the constructor default, dense: lane-per-env path
