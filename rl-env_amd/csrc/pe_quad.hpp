@@ -135,6 +135,45 @@ __device__ __forceinline__ void quad_rays(const uint64_t* lrow, int lane, int kc
   }
 }
 
+// Runtime-(C, R) sector rays: the ray march of pe_step_quad<0, 0, ...> (the table-
+// driven sector kernel of geometries with no compile-time specialization, C <= 32,
+// 2 <= R <= 14).  Wave wv's rays [wv*C/NW, (wv+1)*C/NW); the probe offsets are
+// wave-uniform (the packed (dx & 0xFF | dy << 8) table st.ldxy, R rounded up to 8
+// per ray: scalar loads), so a probe is one LDS read of the window row at the lane's
+// row offset, a shift and the same 2-bit packing as quad_rays (first hit by one
+// find-first-set; plantos_env.py:260-292).
+template <typename OT>
+__device__ __forceinline__ void quad_rays_rt(const uint64_t* lrow, const int16_t* ldxy, int i0, int i1, int R,
+                                             int lane, int kc, int sh, bool watered, OT* row, const float* tdist) {
+  const int RP = (R + 7) & ~7;
+  const uint32_t kNZ = 0x55555555u & ((1u << (2 * R)) - 1u);
+  const float4* tone = reinterpret_cast<const float4*>(tdist + kOneHotF);
+  const uint64_t wclr = ~((uint64_t)(watered ? 1u : 0u) << (sh + 2 * R));  // the rover's cell: 3 -> 2 (watered)
+  for (int i = i0; i < i1; ++i) {
+    const int16_t* o = ldxy + i * RP;
+    uint32_t pk = 0u;
+    for (int r = 0; r < R; ++r) {
+      const int v = o[r];
+      const int dx = (int)(int8_t)(v & 0xFF), dy = (int)(int8_t)((v >> 8) & 0xFF);
+      uint64_t w = lrow[(kc + dx) * kQuadEnvs + lane];
+      if (dx == 0) w &= wclr;  // (uniform)
+      pk |= (uint32_t)((w >> (sh + 2 * (dy + R))) & 3u) << (2 * r);
+    }
+    const uint32_t nz = ((pk | (pk >> 1)) & kNZ) | (1u << (2 * R));
+    const int f = __builtin_ctz(nz);        // 2r of the first hit, 2R if none
+    const int ent = (int)((pk >> f) & 3u);  // its code (EMPTY if none)
+    if constexpr (std::is_same<OT, float>::value) {
+      const float dv = tdist[(f >> 1) + 1];
+      const float4 ov = tone[ent];
+      row[5 * i] = dv;
+      row[5 * i + 1] = ov.x;
+      row[5 * i + 2] = ov.y;
+      row[5 * i + 3] = ov.z;
+      row[5 * i + 4] = ov.w;
+    }
+  }
+}
+
 // Wave-uniform dispatch of the sector code (wv comes from readfirstlane).
 template <int C, int R, int NW, int W = 0, typename T>
 __device__ __forceinline__ void sector_rays(int wv, const uint64_t* lrow, int lane, int kc, int sh, bool watered,

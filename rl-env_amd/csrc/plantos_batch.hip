@@ -574,6 +574,11 @@ template <int R>
 constexpr int quad_tile_off() {
   return (kTabFloats + (2 * R + 3) * kQuadEnvs * 2 + 7 * kQuadEnvs + 3) & ~3;
 }
+// the runtime sector kernel (pe_step_quad<0, 0, ...>): maxima and its layout
+constexpr int kRtCMax = 32, kRtRMax = 14;
+__host__ __device__ constexpr int quad_tile_off_rt(int R) {
+  return (kTabFloats + (2 * R + 3) * kQuadEnvs * 2 + 7 * kQuadEnvs + 3) & ~3;
+}
 // byte-coded tile (BT): the code table ctab[256] after the [64 x D] code tile
 template <int R, int C>
 constexpr int quad_ctab_off() {
@@ -910,22 +915,30 @@ __device__ __forceinline__ void quad_done_obs(const void* ka, int tile_off, int 
 // LDS layout keeps the 64-env stride LS whatever EPB.
 template <int C, int R, bool ONEWORD, int NW, bool BT = false, int EPB = kQuadEnvs>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs (small-batch EPB: one workgroup per CU, no cap); NW=4: <= 128 VGPRs (4 workgroups per CU: G=25 13.1 -> 10.5 us; 1-word C16: 122 -> 104 VGPRs)
-  constexpr int NR = 2 * R + 3, NV = 7, LS = kQuadEnvs, CW = NW - 1;  // CW: commit wave
+  // C == 0 (R == 0): the runtime-(C, R) sector kernel (quad_rays_rt): C, R from the
+  // geometry (up to kRtCMax / kRtRMax), the LDS layout sized at run time
+  constexpr bool RT = C == 0;
+  constexpr int CM = RT ? kRtCMax : C, RM = RT ? kRtRMax : R;
+  static_assert(!RT || (R == 0 && !BT && NW == 4 && EPB == kQuadEnvs), "runtime sector kernel: 4 waves, f32 tile");
+  const int Cr = RT ? a.g.C : C, Rr = RT ? a.g.R : R;
+  constexpr int NR = 2 * RM + 3, NV = 7, LS = kQuadEnvs, CW = NW - 1;  // CW: commit wave
+  const int NRL = RT ? 2 * Rr + 3 : NR;  // window rows (the LDS layout's)
+  const int tile_off = RT ? quad_tile_off_rt(Rr) : quad_tile_off<RM>();
   static_assert(EPB == 16 || EPB == 32 || EPB == 64, "envs per workgroup");
   static_assert(!BT || EPB == kQuadEnvs, "the byte-coded kernel's LDS-DMA staging predicts over all 64 lanes");
 
-  static_assert(C >= NW, "every wave owns a sector of at least one ray");
-  static_assert(ONEWORD || R <= 14, "funnel-shifted window row must hold 2R+5 cells");
-  static_assert(ONEWORD || R >= 2, "the watered cell's byte must lie in the window row");
+  static_assert(RT || C >= NW, "every wave owns a sector of at least one ray");
+  static_assert(ONEWORD || RM <= 14, "funnel-shifted window row must hold 2R+5 cells");
+  static_assert(ONEWORD || RT || R >= 2, "the watered cell's byte must lie in the window row");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* tdist = smem;
   float* tpos = smem + 72;
   float* tvis = smem + 328;
   uint64_t* lrow = reinterpret_cast<uint64_t*>(smem + kTabFloats);  // [NR][LS]
-  uint32_t* lvis = reinterpret_cast<uint32_t*>(lrow + NR * LS);    // [NV][LS]
+  uint32_t* lvis = reinterpret_cast<uint32_t*>(lrow + NRL * LS);   // [NV][LS]
   using OT = typename std::conditional<BT, uint8_t, float>::type;
-  OT* rows = reinterpret_cast<OT*>(smem + quad_tile_off<R>());     // [LS][D] floats or codes
-  float* ctab = smem + quad_ctab_off<R, C>();                       // BT: code -> float
+  OT* rows = reinterpret_cast<OT*>(smem + tile_off);                // [LS][D] floats or codes
+  float* ctab = smem + quad_ctab_off<RM, CM>();                     // BT: code -> float
   const Geo& g = a.g;
   const Rules& rl = a.rl;
   const State& st = a.st;
@@ -961,8 +974,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // one-word rows (G <= 20): the loader env's whole grid block (gstride / 2 <= 10
   // 16-B units, contiguous, 3 per loader thread) comes in round 1 -- its address does
   // not depend on the position -- and only the visit rows are left for round 2
-  // gstride / 2 16-B units: one-word rows need G + 2R <= 32 (C16R6: G <= 20, 10 units)
-  constexpr int JG1 = ((32 - 2 * R + 1) / 2 + LT - 1) / LT;
+  constexpr int JG1 = (10 + LT - 1) / LT;  // gstride / 2 <= 10 16-B units (one-word: NW == 4, G <= 20)
   constexpr bool kGridR1 = ONEWORD && PE_GRID_R1;
   uint4 qg1[kGridR1 ? JG1 : 1];
   if constexpr (kGridR1) {
@@ -1001,13 +1013,13 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
     uint32_t acc = 0;
     for (int k = threadIdx.x; k < ng; k += blockDim.x) acc ^= gsrc[k].x ^ gsrc[k].w;
     for (int k = threadIdx.x; k < nv; k += blockDim.x) acc ^= vsrc[k].y ^ vsrc[k].z;
-    reinterpret_cast<uint32_t*>(smem + quad_tile_off<R>())[threadIdx.x] = acc;
+    reinterpret_cast<uint32_t*>(smem + tile_off)[threadIdx.x] = acc;
   }
-  load_tables_hot(smem, st.tab, a.g.G, R);
+  load_tables_hot(smem, st.tab, a.g.G, Rr);
   // the sector rays' tables (pe_quad.hpp quad_rays): dist[R+1] = 1.0, one-hot rows
-  static_assert(R + 2 <= kOneHotF && kOneHotF + 16 <= 70, "ray tables inside dist[], below the done mask");
+  static_assert(RM + 2 <= kOneHotF && kOneHotF + 16 <= 70, "ray tables inside dist[], below the done mask");
   if (threadIdx.x < 16) smem[kOneHotF + threadIdx.x] = (threadIdx.x >> 2) == (threadIdx.x & 3) ? 1.0f : 0.0f;
-  if (threadIdx.x == 16) smem[R + 1] = 1.0f;
+  if (threadIdx.x == 16) smem[Rr + 1] = 1.0f;
   if constexpr (BT) {
     if (threadIdx.x < 256) ctab[threadIdx.x] = obs_code_value(st.tab, R, g.G, (int)threadIdx.x);
   }
@@ -1044,7 +1056,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // only (64x64 desynchronized: 36.6 -> 36.2 us): at 20x20 the waits hipcc places
   // around a possibly outstanding LDS-DMA (a vmcnt(0) at the next use of any load
   // result) serialize round 2 in every block (9.39 -> 10.0 us, desync 11.52 -> 12.29).
-  float* stage = smem + (BT ? quad_ctab_off<R, C>() + 256 : quad_tile_off<R>() + LS * (5 * C + 27));
+  float* stage = smem + (BT ? quad_ctab_off<RM, CM>() + 256 : tile_off + LS * (5 * Cr + 27));
   const bool stage_ok = BT && a.pf.scal && quad_coop(a, 1) && e0 + EPB <= a.n;  // full block: every lane live
   const bool stage_info = !st.cur && a.tinfo && pf_stage_info_fits(g.G, g.WPR, (int)a.pf.ostride);
   // (issued right after round 2's own loads: hipcc drains every memory op in flight
@@ -1075,7 +1087,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // instead, the done path's first use waited for the commit's stores too (vmcnt
   // counts both, in order).  (The byte-coded kernel stages the same record by
   // LDS-DMA during round 2.)
-  constexpr int KDQ = (5 * C + 27 + 63) / 64, MAXWQ = ONEWORD ? 1 : kCoopWPR;
+  constexpr int KDQ = (5 * CM + 27 + 63) / 64, MAXWQ = ONEWORD ? 1 : kCoopWPR;
   // (one-word 64-env kernels only: the multi-word kernel is at its 128-VGPR cap and
   // spilled with it -- 25x25 desynchronized 14.0 -> 14.6 us -- and the 16-env shape of
   // small batches lost 2-5 % synchronized; profiles/r3c_ab_early_*.jsonl)
@@ -1104,7 +1116,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   if (llive && !(kAblate & 4)) {
     const int lx = (int)(lw.x & 0xFF), ly = (int)((lw.x >> 8) & 0xFF);
     const uint64_t* lgb = st.grid + el * g.gstride;
-    const int base = lx - R - 1;  // grid row of LDS row 0
+    const int base = lx - Rr - 1;  // grid row of LDS row 0
     // Every load first, then the LDS writes: the loads are unconditional (row
     // indices clamped into the map, off-map rows selected away afterwards), so the
     // compiler issues all of them back to back and waits once -- with the range
@@ -1144,14 +1156,14 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
           if (q < nq) {
             const uint64_t lo = (uint64_t)qg1[j].x | ((uint64_t)qg1[j].y << 32);
             const uint64_t hi = (uint64_t)qg1[j].z | ((uint64_t)qg1[j].w << 32);
-            if (ka >= 0 && ka < NR) lrow[ka * LS + le] = lo;
-            if (ka + 1 >= 0 && ka + 1 < NR && 2 * q + 1 < g.G) lrow[(ka + 1) * LS + le] = hi;
+            if (ka >= 0 && ka < NRL) lrow[ka * LS + le] = lo;
+            if (ka + 1 >= 0 && ka + 1 < NRL && 2 * q + 1 < g.G) lrow[(ka + 1) * LS + le] = hi;
           }
         }
 #pragma unroll
         for (int j = 0; j < (NR + LT - 1) / LT; ++j) {
           const int k = sub + LT * j, xr = base + k;
-          if (k < NR && (xr < 0 || xr >= g.G)) lrow[k * LS + le] = kEven64;  // off-map rows: obstacles
+          if (k < NRL && (xr < 0 || xr >= g.G)) lrow[k * LS + le] = kEven64;  // off-map rows: obstacles
         }
       }
 #pragma unroll
@@ -1166,8 +1178,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
           const uint64_t va = (ra >= 0 && ra < g.G) ? (ra == rc ? lo : hi) : kEven64;
           const uint64_t vb2 = (ra + 1 >= 0 && ra + 1 < g.G) ? (ra + 1 == rc ? lo : hi) : kEven64;
           const int ka = ra - base;
-          if (ka >= 0 && ka < NR) lrow[ka * LS + le] = va;
-          if (ka + 1 >= 0 && ka + 1 < NR) lrow[(ka + 1) * LS + le] = vb2;
+          if (ka >= 0 && ka < NRL) lrow[ka * LS + le] = va;
+          if (ka + 1 >= 0 && ka + 1 < NRL) lrow[(ka + 1) * LS + le] = vb2;
         }
       }
       // visit rows: one 16-B row per load, funnel-shifted to ybv
@@ -1242,31 +1254,19 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
       }
       const int lybv = ly > 0 ? ly - 1 : 0;
       const int vw = (4 * lybv) >> 5, vo = (4 * lybv) & 31;
-      if (g.NW == 4) {  // (G <= 25) 16-B rows: one load per row, words vw, vw + 1 <= 3 selected
-        const uint4* vq = reinterpret_cast<const uint4*>(st.vis + el * g.vstride);
+      const uint32_t* vb = st.vis + el * g.vstride + vw;
 #pragma unroll
-        for (int j = 0; j < JV; ++j) {
-          const int xr = lx - 3 + sub + LT * j;
-          const int xc = xr < 0 ? 0 : (xr >= g.G ? g.G - 1 : xr);
-          const uint4 q = vq[xc];
-          vlo[j] = vw == 0 ? q.x : (vw == 1 ? q.y : q.z);
-          vhi[j] = vw == 0 ? q.y : (vw == 1 ? q.z : q.w);
-        }
-      } else {
-        const uint32_t* vb = st.vis + el * g.vstride + vw;
-#pragma unroll
-        for (int j = 0; j < JV; ++j) {
-          const int xr = lx - 3 + sub + LT * j;
-          const int xc = xr < 0 ? 0 : (xr >= g.G ? g.G - 1 : xr);
-          vlo[j] = vb[(int64_t)xc * g.NW];
-          vhi[j] = vb[(int64_t)xc * g.NW + 1];  // vw + 1 < NW always (one spare word per row)
-        }
+      for (int j = 0; j < JV; ++j) {
+        const int xr = lx - 3 + sub + LT * j;
+        const int xc = xr < 0 ? 0 : (xr >= g.G ? g.G - 1 : xr);
+        vlo[j] = vb[(int64_t)xc * g.NW];
+        vhi[j] = vb[(int64_t)xc * g.NW + 1];  // vw + 1 < NW always (one spare word per row)
       }
       stage_issue();
 #pragma unroll
       for (int j = 0; j < JG; ++j) {
         const int k = sub + LT * j;
-        if (k < NR) {
+        if (k < NRL) {
           const int xr = base + k;
           uint64_t v = kEven64;  // off-map rows read as obstacles
           if (xr >= 0 && xr < g.G) {
@@ -1331,8 +1331,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   int dxv = 0;
   double h = 0.0;
   if (mv) {
-    const uint64_t rt = lrow[(R + 1 + dxm) * LS + lane];
-    ok = inb && ((rt >> (2 * (nyc + R - yb))) & 3u) != OBST;      // :193-195 (plants walkable)
+    const uint64_t rt = lrow[(Rr + 1 + dxm) * LS + lane];
+    ok = inb && ((rt >> (2 * (nyc + Rr - yb))) & 3u) != OBST;     // :193-195 (plants walkable)
     if (ok) {
       n = (lvis[(3 + dxm) * LS + lane] >> (4 * (nyc + 2 - ybv))) & 15u;
       h = n == 0u ? rl.r_exploration : rl.r_revisit;              // :197, 204-207
@@ -1343,8 +1343,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
       h = rl.r_invalid;                                           // :211
     }
   } else if (water) {
-    const uint64_t rc = lrow[(R + 1) * LS + lane];
-    const int cd = (int)((rc >> (2 * (s.y + R - yb))) & 3u);
+    const uint64_t rc = lrow[(Rr + 1) * LS + lane];
+    const int cd = (int)((rc >> (2 * (s.y + Rr - yb))) & 3u);
     if (cd == THIRSTY) {                                          // fork plantos_env_new.py:237-240
       watered = true;
       h = rl.r_goal;
@@ -1360,20 +1360,24 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   OT* row = rows + lane * g.D;
   bool done = false, wfix = false;
   if (live) {
-    const int kc = dxv + R + 1;
+    const int kc = dxv + Rr + 1;
     const int sh = 2 * (yp - yb);
     const int vs = 4 * (yp - ybv);
-    if constexpr (!(kAblate & 2)) sector_rays<C, R, NW>(wv, lrow, lane, kc, sh, watered, row, tdist);
+    if constexpr (RT) {
+      quad_rays_rt<OT>(lrow, st.ldxy, wv * Cr / NW, (wv + 1) * Cr / NW, Rr, lane, kc, sh, watered, row, tdist);
+    } else if constexpr (!(kAblate & 2)) {
+      sector_rays<C, R, NW>(wv, lrow, lane, kc, sh, watered, row, tdist);
+    }
     // slice rows and position go to the non-commit waves (the commit wave is the laggard)
     if (wv != CW)
-      for (int lx = wv; lx < 5; lx += NW - 1) quad_slice_row(lvis, lane, lx, dxv, vs, ok, nib, C, row, tvis);
+      for (int lx = wv; lx < 5; lx += NW - 1) quad_slice_row(lvis, lane, lx, dxv, vs, ok, nib, Cr, row, tvis);
     if (wv == (NW == 4 ? 2 : 5)) {                                // :294-296
       if constexpr (BT) {
-        row[5 * C] = (uint8_t)(kCodePos + xp);
-        row[5 * C + 1] = (uint8_t)(kCodePos + yp);
+        row[5 * Cr] = (uint8_t)(kCodePos + xp);
+        row[5 * Cr + 1] = (uint8_t)(kCodePos + yp);
       } else {
-        row[5 * C] = tpos[xp];
-        row[5 * C + 1] = tpos[yp];
+        row[5 * Cr] = tpos[xp];
+        row[5 * Cr + 1] = tpos[yp];
       }
     }
     if (wv == CW && !(kAblate & 8)) {
@@ -1437,14 +1441,14 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
           }
         }
         if (watered) {
-          const int bit = 2 * (s.y + R);
+          const int bit = 2 * (s.y + Rr);
           if constexpr (ONEWORD) {
-            st_wt(const_cast<uint64_t*>(gb) + ox, (uint64_t)(lrow[(R + 1) * LS + lane] & ~(1ull << bit)));  // code 3 -> 2
+            st_wt(const_cast<uint64_t*>(gb) + ox, (uint64_t)(lrow[(Rr + 1) * LS + lane] & ~(1ull << bit)));  // code 3 -> 2
           } else {
             // the byte holding the cell's code (padded column c; its 4 cells lie in the
             // window of row x, padded columns yb..yb+31, for R >= 2)
-            const int c = s.y + R, B = c >> 2;
-            const uint64_t wr = lrow[(R + 1) * LS + lane] & ~(1ull << (2 * (c - yb)));  // code 3 -> 2
+            const int c = s.y + Rr, B = c >> 2;
+            const uint64_t wr = lrow[(Rr + 1) * LS + lane] & ~(1ull << (2 * (c - yb)));  // code 3 -> 2
             st_wt(reinterpret_cast<uint8_t*>(const_cast<uint64_t*>(gb) + (int64_t)ox * g.WPR) + B,
                   (uint8_t)(wr >> (2 * (4 * B - yb))));
           }
@@ -1469,7 +1473,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // ---- DummyVecEnv auto-reset (rare): commit wave, after the whole obs row is in LDS
   // any env of the block done (the usual answer: no)?  The commit wave's done mask
   // goes to an unused LDS table word (dist[70..71]) for the count the reset path needs.
-  static_assert(R < 70, "dist[70..71] holds the done mask");
+  static_assert(RM < 70, "dist[70..71] holds the done mask");
   if (wv == CW) {
     const uint64_t dm = __ballot(done);
     if (lane == 0) reinterpret_cast<uint64_t*>(smem)[35] = dm;
@@ -1487,13 +1491,14 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   const int ndone = __popcll(dmu);
   PE_STAMP(5);
   // auto-reset slow path, out of line (its registers stay off the hot path)
-  static_assert(2 * C * R <= (NR * 8 + NV * 4) * LS, "LIDAR offset tables must fit the window region");
-  static_assert(5 * 4 * LS + 8 <= (NR * 8 + NV * 4) * LS, "reset staging must fit the window region");
+  // (RT: the region is sized by the actual R -- pe_create checks these at run time)
+  static_assert(RT || 2 * C * R <= (NR * 8 + NV * 4) * LS, "LIDAR offset tables must fit the window region");
+  static_assert(RT || 5 * 4 * LS + 8 <= (NR * 8 + NV * 4) * LS, "reset staging must fit the window region");
   const int64_t valid = a.n - e0 < EPB ? a.n - e0 : EPB;
   if (__builtin_expect(any_done, 0)) {  // cold: laid out after the hot path
     const bool staged = stage_ok && npred == 1 && ndone == 1;  // then the done env is the predicted one
-    const uint4 ns = quad_done_path<NW, ONEWORD, (5 * C + 27 + 63) / 64, BT>(
-        kernargs(), quad_tile_off<R>(), C, R, lane, wv, CW, e0, done, pack(s), ret, ndone, wfix, ctab,
+    const uint4 ns = quad_done_path<NW, ONEWORD, (5 * CM + 27 + 63) / 64, BT>(
+        kernargs(), tile_off, Cr, Rr, lane, wv, CW, e0, done, pack(s), ret, ndone, wfix, ctab,
         staged ? stage : nullptr, staged && stage_info, e_early, &epl, &eir);
     s = unpack(ns);
   }
@@ -1502,7 +1507,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // would make every iteration of its store loop wait for them (s_waitcnt vmcnt(0)
   // before re-using a store's data registers)
   if constexpr (!(kAblate & 1)) {
-    if constexpr (C >= 64) {  // long rows: the commit wave's share pays for its wait (64x64: 33.2 -> 32.7 us)
+    if constexpr (CM >= 64) {  // long rows: the commit wave's share pays for its wait (64x64: 33.2 -> 32.7 us)
       if (wv == CW) __builtin_amdgcn_s_waitcnt(0x0F70);  // tracked vmcnt(0): no wait inside the loop
       if constexpr (BT)
         store_tile_codes(rows, ctab, a.obs + e0 * g.D, (int)valid, g.D, (int)threadIdx.x, (int)blockDim.x);
@@ -1523,7 +1528,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
     // from the grid image (LDS scratch, or BT: the env's rows in HBM)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    quad_done_obs<NW, BT>(kernargs(), quad_tile_off<R>(), lane, e, done, pack(s));
+    quad_done_obs<NW, BT>(kernargs(), tile_off, lane, e, done, pack(s));
   }
   PE_STAMP(6);
 #ifdef PE_STAMPS
@@ -2377,7 +2382,8 @@ enum Variant {
   V_GENERIC = 0, V_C16R6_1W = 1, V_C16R6 = 2, V_C64R6 = 3,
   V_QUAD_C16R6_1W = 4, V_QUAD_C16R6 = 5, V_QUAD_C64R6 = 6,
   V_QUAD_C10R2_1W = 7, V_QUAD_C10R2 = 8,  // plantos_env.py:25-26 constructor default (G=21: multi-word)
-  V_QUAD_C16R4_1W = 9, V_QUAD_C16R4 = 10  // test_environment.py:24 (G=15, C=16, R=4)
+  V_QUAD_C16R4_1W = 9, V_QUAD_C16R4 = 10,  // test_environment.py:24 (G=15, C=16, R=4)
+  V_QUAD_RT_1W = 11, V_QUAD_RT = 12        // runtime (C, R): every other geometry with C <= 32, 2 <= R <= 14
 };
 
 // the prefetched records' obs row stride (bytes; pe_device.hpp Prefetch)
@@ -2424,6 +2430,8 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
       case V_QUAD_C10R2_1W: PE_QUAD4(10, 2, true); break;
       case V_QUAD_C10R2: PE_QUAD4(10, 2, false); break;
       case V_QUAD_C16R4_1W: PE_QUAD4(16, 4, true); break;
+      case V_QUAD_RT_1W: PE_QUAD4(0, 0, true); break;
+      case V_QUAD_RT: PE_QUAD4(0, 0, false); break;
       default: PE_QUAD4(16, 4, false); break;
     }
 #undef PE_QUAD
@@ -2526,6 +2534,8 @@ const char* variant_name(int v) {
     case V_QUAD_C10R2: return "pe_step_quad<C10,R2>";
     case V_QUAD_C16R4_1W: return "pe_step_quad<C16,R4,1word>";
     case V_QUAD_C16R4: return "pe_step_quad<C16,R4>";
+    case V_QUAD_RT_1W: return "pe_step_quad<runtime C,R,1word>";
+    case V_QUAD_RT: return "pe_step_quad<runtime C,R>";
     default: return "pe_step_wave";
   }
 }
@@ -2617,10 +2627,11 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   g.WPR = (2 * (G + 2 * R) + 63) / 64;
   // visit row words: the padded row's G+4 nibbles + a spare word, so that the 8-nibble
   // window starting at any padded column y-1 (words vw, vw+1) stays inside the row.
-  // Up to G = 25, 4 words already do (vw <= 2): 16-B rows, one dwordx4 per window row
-  // in the sector kernels (the reference's training grid, 25x25, and the constructor
-  // default's 21x21 included)
-  g.NW = G <= 25 ? 4 : (4 * (G + 4) + 31) / 32 + 1;
+  // (Tried: 4 words up to G = 25 -- 16-B rows, one load per window row in the
+  // multi-word kernel: 25x25 10.38 -> 10.97 us, 21x21/C10/R2 one-word 8.05 -> 8.14;
+  // profiles/r3j_ab_*.jsonl.)
+  g.NW = (4 * (G + 4) + 31) / 32 + 1;
+  if (g.NW < 4) g.NW = 4;  // 16-B visit rows: one dwordx4 per row in the sector kernel
   g.EW = (g.GG + 31) / 32;
   g.gstride = (int64_t)align_up((size_t)G * g.WPR, 2);  // 16-B aligned env blocks (row-pair loads)
   g.vstride = (int64_t)G * g.NW;
@@ -2718,9 +2729,14 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   if (!lane_kernels && C == 16 && R == 4 && table_matches<16, 4>(ldx, ldy)) h->variant = V_QUAD_C16R4_1W;
   if (h->variant >= V_QUAD_C10R2_1W) h->quad_waves = 4;
   // the one-word form (whole padded row in one u64) needs WPR == 1 and 16-B visit
-  // rows (NW == 4: G <= 25); otherwise the multi-word (funnel-shifted) form
+  // rows (NW == 4: G <= 20); otherwise the multi-word (funnel-shifted) form
   const bool oneword = g.WPR == 1 && g.NW == 4;
   if ((h->variant == V_QUAD_C10R2_1W || h->variant == V_QUAD_C16R4_1W) && !oneword) h->variant += 1;
+  // every other geometry with 4 <= C <= 32 and 2 <= R <= 14: the sector kernel with
+  // table-driven rays (quad_rays_rt) instead of one wave per env -- 64 envs per
+  // workgroup share the per-env work the wave kernel repeats per wave
+  if (!lane_kernels && h->variant == V_GENERIC && C >= 4 && C <= kRtCMax && R >= 2 && R <= kRtRMax)
+    h->variant = oneword ? V_QUAD_RT_1W : V_QUAD_RT;
   if (h->variant == V_QUAD_C16R6_1W && g.NW != 4) h->variant = V_C16R6_1W;  // needs 16-B visit rows
   // byte-coded obs tile where the f32 tile limits the sector kernel's occupancy
   // (C = 64: 89 KB -> 22 KB of LDS per workgroup)

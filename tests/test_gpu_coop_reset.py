@@ -18,14 +18,15 @@ pytestmark = pytest.mark.gpu
 CFG = {
     "g20": (20, 10, 12, 6, 16),
     "g64": (64, 100, 120, 6, 64),
-    "g7": (7, 3, 3, 3, 12),
-    "g32": (32, 20, 30, 9, 24),
+    "g7": (7, 3, 3, 3, 12),        # runtime sector kernel, one-word
+    "g32": (32, 20, 30, 9, 24),    # runtime sector kernel, multi-word
     "g21": (21, 8, 50, 2, 10),
     "g25": (25, 10, 12, 6, 16),   # the multi-word C16 sector kernel (train_mcts's grid)
     "g15": (15, 6, 8, 4, 16),     # one-word C16R4 sector kernel (test_environment.py:24)
     "g12r2": (12, 4, 6, 2, 10),   # one-word C10R2
     "g64r32": (64, 100, 120, 32, 64),  # the one-wave-per-env kernel (long rays)
     "g30r2": (30, 12, 40, 2, 10),  # multi-word C10R2
+    "g16c40": (16, 6, 8, 5, 40),   # C > 32: the one-wave-per-env kernel
 }
 
 
@@ -52,6 +53,7 @@ def info_rows(b, idx):
     ("g15", 600, 80, 60, None, None, None, None, False),
     ("g12r2", 600, 80, 60, None, None, None, None, False),
     ("g30r2", 400, 60, 50, None, None, None, None, False),
+    ("g16c40", 300, 60, 50, None, None, None, None, False),
     ("g64r32", 192, 50, 40, None, None, None, None, False),
     ("g64r32", 128, 12, 1, "0", None, None, None, False),    # dense: serial resets (coop_max_done 0)
     ("g21", 256, 12, 1, "0", None, None, None, False),        # the constructor default, dense: lane-per-env path

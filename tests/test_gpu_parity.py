@@ -23,9 +23,11 @@ CFG = {
     "g32": (32, 20, 30, 9, 24),
     "g15": (15, 6, 8, 4, 16),     # test_environment.py:24's custom env (one-word C16R4 sector kernel)
     "g25r4": (25, 10, 12, 4, 16),  # multi-word C16R4
-    "g12r2": (12, 4, 6, 2, 10),    # one-word C10R2 (as g21, the constructor default)
+    "g12r2": (12, 4, 6, 2, 10),    # one-word C10R2 (g21 = the constructor default: multi-word C10R2)
     "g30r2": (30, 12, 40, 2, 10),  # multi-word C10R2 (G + 2R > 32)
-    "g8r12": (8, 3, 3, 12, 16),    # R > G: the wave kernel's raw-window ray path (no rover-aligned re-staging)
+    "g8r12": (8, 3, 3, 12, 16),    # R > G: runtime sector kernel, window rows mostly off the map
+    "g8r20": (8, 3, 3, 20, 16),    # R > 14 and > G: the wave kernel's raw-window ray path (no rover-aligned re-staging)
+    "g16c40": (16, 6, 8, 5, 40),   # C > 32: the wave kernel (rover-aligned window)
     "g24c100": (24, 10, 12, 8, 100),  # C = 100 (near the 120-ray LDS bound): wave kernel, rays past lane 63
 }
 
@@ -33,9 +35,10 @@ CFG = {
 # specialization exists, the table-driven kernel otherwise
 KERNELS = {
     "g20": "pe_step_quad<C16,R6,1word>", "g25": "pe_step_quad<C16,R6>", "g64": "pe_step_quad<C64,R6>",
-    "g21": "pe_step_quad<C10,R2,1word>", "g12r2": "pe_step_quad<C10,R2,1word>", "g30r2": "pe_step_quad<C10,R2>", "g15": "pe_step_quad<C16,R4,1word>",
-    "g25r4": "pe_step_quad<C16,R4>", "g64r32": "pe_step_wave", "g7": "pe_step_wave",
-    "g32": "pe_step_wave", "g8r12": "pe_step_wave", "g24c100": "pe_step_wave",
+    "g21": "pe_step_quad<C10,R2>", "g12r2": "pe_step_quad<C10,R2,1word>", "g30r2": "pe_step_quad<C10,R2>", "g15": "pe_step_quad<C16,R4,1word>",
+    "g25r4": "pe_step_quad<C16,R4>", "g64r32": "pe_step_wave", "g7": "pe_step_quad<runtime C,R,1word>",
+    "g32": "pe_step_quad<runtime C,R>", "g8r12": "pe_step_quad<runtime C,R,1word>", "g24c100": "pe_step_wave",
+    "g8r20": "pe_step_wave", "g16c40": "pe_step_wave",
 }
 
 
@@ -174,7 +177,7 @@ def test_small_batch_workgroup_shape(n, suffix):
                                           ("g64", 256, 120), ("g64r32", 96, 60), ("g25", 300, 200),
                                           ("g15", 1000, 1010), ("g25r4", 300, 200), ("g12r2", 500, 300),
                                           ("g32", 400, 300), ("g8r12", 300, 300), ("g24c100", 200, 120),
-                                          ("g30r2", 300, 200)])
+                                          ("g30r2", 300, 200), ("g8r20", 300, 200), ("g16c40", 300, 200)])
 def test_rollout_parity_device_rng(name, n, steps):
     """Device-rng episodes with synthetic actions, auto-reset included (g20 crosses
     the 1000-step truncation): every output of every step vs the oracle."""
