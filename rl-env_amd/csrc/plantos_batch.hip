@@ -970,7 +970,9 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   const int32_t* ap = reinterpret_cast<const int32_t*>(a.actions);
   const int32_t alo = ap[ec << ash], ahi = ap[(ec << ash) + ash];
   double ret = st.ep_ret[wv == CW ? ec : 0];  // (the commit wave's; the others read one shared word)
-  const uint4 lw = st.scal[elc];
+  // (the loader env's scalars are not loaded again: lane le of this wave holds them --
+  // every wave loads the block's 64 records in its lane role -- and a bpermute moves
+  // the position word over once round 1 has landed)
   // one-word rows (G <= 20): the loader env's whole grid block (gstride / 2 <= 10
   // 16-B units, contiguous, 3 per loader thread) comes in round 1 -- its address does
   // not depend on the position -- and only the visit rows are left for round 2
@@ -1026,7 +1028,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   const Tables* ltab = reinterpret_cast<const Tables*>(smem);
   Scal s = unpack(sw);
 #ifdef PE_STAMPS
-  if ((int)(s.x + lw.x) == -12345) g_stamps[0] = 1;  // consume round 1 before the stamp
+  if ((int)(s.x + sw.y) == -12345) g_stamps[0] = 1;  // consume round 1 before the stamp
 #endif
   PE_STAMP(1);
   const int64_t action = ash ? (int64_t)(((uint64_t)(uint32_t)ahi << 32) | (uint32_t)alo) : (int64_t)alo;
@@ -1113,8 +1115,11 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   }
   // ---- round 2: window rows of env le -> LDS [row][env] (loader role)
   uint32_t eo = 0u, en = 0u;
+  // env le = lane le of this wave (le < EPB <= 64); outside the branch below: a
+  // bpermute must run on every lane (it reads the source lane's register)
+  const uint32_t lwx = (uint32_t)__shfl((int)sw.x, le);
   if (llive && !(kAblate & 4)) {
-    const int lx = (int)(lw.x & 0xFF), ly = (int)((lw.x >> 8) & 0xFF);
+    const int lx = (int)(lwx & 0xFF), ly = (int)((lwx >> 8) & 0xFF);
     const uint64_t* lgb = st.grid + el * g.gstride;
     const int base = lx - Rr - 1;  // grid row of LDS row 0
     // Every load first, then the LDS writes: the loads are unconditional (row
