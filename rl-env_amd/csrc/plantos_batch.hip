@@ -970,9 +970,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   const int32_t* ap = reinterpret_cast<const int32_t*>(a.actions);
   const int32_t alo = ap[ec << ash], ahi = ap[(ec << ash) + ash];
   double ret = st.ep_ret[wv == CW ? ec : 0];  // (the commit wave's; the others read one shared word)
-  // (the loader env's scalars are not loaded again: lane le of this wave holds them --
-  // every wave loads the block's 64 records in its lane role -- and a bpermute moves
-  // the position word over once round 1 has landed)
+  // (Tried: the loader env's position by a bpermute from lane le of the wave instead of
+  // this load -- 64x64 24.5 -> 25.2 us, 25x25 desync +0.4 us, the headline unchanged;
+  // profiles/r3m_ab_*.jsonl.)
+  const uint4 lw = st.scal[elc];
   // one-word rows (G <= 20): the loader env's whole grid block (gstride / 2 <= 10
   // 16-B units, contiguous, 3 per loader thread) comes in round 1 -- its address does
   // not depend on the position -- and only the visit rows are left for round 2
@@ -1028,7 +1029,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   const Tables* ltab = reinterpret_cast<const Tables*>(smem);
   Scal s = unpack(sw);
 #ifdef PE_STAMPS
-  if ((int)(s.x + sw.y) == -12345) g_stamps[0] = 1;  // consume round 1 before the stamp
+  if ((int)(s.x + lw.x) == -12345) g_stamps[0] = 1;  // consume round 1 before the stamp
 #endif
   PE_STAMP(1);
   const int64_t action = ash ? (int64_t)(((uint64_t)(uint32_t)ahi << 32) | (uint32_t)alo) : (int64_t)alo;
@@ -1115,11 +1116,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   }
   // ---- round 2: window rows of env le -> LDS [row][env] (loader role)
   uint32_t eo = 0u, en = 0u;
-  // env le = lane le of this wave (le < EPB <= 64); outside the branch below: a
-  // bpermute must run on every lane (it reads the source lane's register)
-  const uint32_t lwx = (uint32_t)__shfl((int)sw.x, le);
   if (llive && !(kAblate & 4)) {
-    const int lx = (int)(lwx & 0xFF), ly = (int)((lwx >> 8) & 0xFF);
+    const int lx = (int)(lw.x & 0xFF), ly = (int)((lw.x >> 8) & 0xFF);
     const uint64_t* lgb = st.grid + el * g.gstride;
     const int base = lx - Rr - 1;  // grid row of LDS row 0
     // Every load first, then the LDS writes: the loads are unconditional (row
@@ -1494,6 +1492,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
                        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(dmask >> 32)) << 32);
   const bool any_done = dmu != 0ull;
   const int ndone = __popcll(dmu);
+  // (Tried: a single-done fast path -- the early record checked before the done barrier,
+  // no barrier after the reset, the commit wave storing its env's chunks of the tile and
+  // the other waves the rest at once: desync 11.14 -> 11.38 us, synchronized 9.46 -> 9.60;
+  // profiles/r3n_ab_*.jsonl.)
   PE_STAMP(5);
   // auto-reset slow path, out of line (its registers stay off the hot path)
   // (RT: the region is sized by the actual R -- pe_create checks these at run time)
@@ -1520,10 +1522,11 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
         store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D);
     } else {
       if (wv != CW) {
-        if constexpr (BT)
+        if constexpr (BT) {
           store_tile_codes(rows, ctab, a.obs + e0 * g.D, (int)valid, g.D, (int)threadIdx.x, 64 * (NW - 1));
-        else
+        } else {
           store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D, (int)threadIdx.x, 64 * (NW - 1));
+        }
       }
     }
   }
