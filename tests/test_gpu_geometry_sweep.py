@@ -1,0 +1,77 @@
+"""A seeded sweep of geometries through every step kernel the library selects: the
+runtime-(C, R) sector kernel (4 <= C <= 32, 2 <= R <= 14, one-word and multi-word
+rows), the compile-time sector kernels, and the one-wave-per-env kernel (C > 32 or
+R > 14) -- each against the oracle (plantos_env.py:160-315 restated), every output
+of every step, episodes desynchronized so that auto-resets happen inside the window,
+the final state included.  Batch sizes are ragged (a partial last workgroup)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from oracle_rollout import OracleVec
+
+pytestmark = pytest.mark.gpu
+
+
+def _geometries():
+    rng = np.random.default_rng(2026)
+    out = []
+    while len(out) < 14:
+        kind = len(out) % 3
+        if kind < 2:  # the runtime sector kernel's range
+            C, R = int(rng.integers(4, 33)), int(rng.integers(2, 15))
+        else:         # the wave kernel's
+            if rng.random() < 0.5:
+                C, R = int(rng.integers(33, 100)), int(rng.integers(1, 12))
+            else:
+                C, R = int(rng.integers(4, 40)), int(rng.integers(15, 30))
+        G = int(rng.integers(5, 41))
+        cells = G * G
+        O_ = int(rng.integers(0, max(1, cells // 10)))
+        P = int(rng.integers(1, max(2, min(40, cells // 8))))
+        # map generation needs room: clusters of <= 9 cells, P plants + the rover
+        if (O_ // 3) * 9 + P + 1 > cells - 4 * G:
+            continue
+        out.append((G, P, O_, R, C))
+    return out
+
+
+GEOS = _geometries()
+
+
+@pytest.mark.parametrize("cfg", GEOS, ids=[f"G{g}P{p}O{o}R{r}C{c}" for g, p, o, r, c in GEOS])
+def test_geometry_sweep_parity(cfg):
+    from plantos_amd import PlantOSBatch
+    G, P, O_, R, C = cfg
+    n, steps, seed = 133, 60, 17
+    b = PlantOSBatch(n, grid_size=G, num_plants=P, num_obstacles=O_, lidar_range=R, lidar_channels=C, seed=seed,
+                     device="cuda:0")
+    rt = 4 <= C <= 32 and 2 <= R <= 14
+    if rt:  # (or a compile-time specialization of the same sector kernel)
+        assert b.kernel_name.startswith("pe_step_quad"), b.kernel_name
+    elif C > 32 or R > 14:
+        assert b.kernel_name == "pe_step_wave", b.kernel_name
+    ov = OracleVec(cfg, np.arange(n), seed)
+    start = (999 - np.random.default_rng(3).integers(0, 40, n)).astype(np.int32)
+    sc = b.get_state(parts=("scalars",))["scalars"].cpu().numpy()
+    sc[:, O.S_STEP] = start
+    b.set_state(scalars=sc)
+    ov.b.scal[:, O.S_STEP] = start
+    act = torch.empty(n, dtype=torch.int32, device="cuda:0")
+    for t in range(steps):
+        b.synth_actions(seed, t, out=act)
+        obs, rew, te, tr = b.step(act)
+        o_obs, o_rew, o_te, o_tr, o_tobs, o_ret, o_len = ov.step(act.cpu().numpy())
+        assert (rew.cpu().numpy() == o_rew.astype(np.float32)).all(), t
+        assert (te.cpu().numpy().astype(bool) == o_te).all() and (tr.cpu().numpy().astype(bool) == o_tr).all(), t
+        assert (obs.cpu().numpy() == o_obs).all(), t
+        done = o_te | o_tr
+        if done.any():
+            assert (b.terminal_obs.cpu().numpy()[done] == o_tobs[done]).all(), t
+            assert (b.episode_return.cpu().numpy()[done] == o_ret[done]).all(), t
+    st = b.get_state()
+    assert (st["cells"].cpu().numpy() == ov.b.cells).all()
+    assert (st["visits"].cpu().numpy() == ov.b.visits).all()
+    assert (st["scalars"].cpu().numpy() == ov.b.scal).all()
+    b.close()
