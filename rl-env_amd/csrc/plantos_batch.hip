@@ -495,34 +495,14 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
   store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.DS);
 }
 
-// Diagnostic phase ablation (tools/ablate.py builds a SEPARATE library with
-// -DPE_ABLATE=bits; the product library is built without it): 1 = no obs tile
-// store, 2 = no ray-march, 4 = no round-2 window loads, 8 = no state commit,
-// 16 = no visit-row loads, 32 = no grid-row loads, 64 = timing probe: the block's
-// whole grid + visit blocks streamed in round 1 (coalesced) instead of round 2.
+// (The round-1 phase ablations and the round-2 timing probes -- PE_ABLATE, PE_PROBE_*,
+// PE_VIS_R1 -- were separate libraries built from this file; their results are in
+// DESIGN.md §8 and profiles/r1d_ablation.json, profiles/r2ag_*; the probes are gone.)
 #ifndef PE_GRID_R1
 #define PE_GRID_R1 1  // one-word sector kernel: the grid block in round 1 (A/B: -DPE_GRID_R1=0)
 #endif
-#ifndef PE_VIS_R1
-#define PE_VIS_R1 0  // ... and the visit block too: no second round (A/B: -DPE_VIS_R1=1)
-#endif
 #ifndef PE_STAGGER_GROUPS
 #define PE_STAGGER_GROUPS 4  // sector kernel: the grid's start-delay groups (A/B: -DPE_STAGGER_GROUPS=n)
-#endif
-#ifndef PE_PROBE_NOVIS
-#define PE_PROBE_NOVIS 0  // timing probe only: constant visit window, no visit-row loads
-#endif
-#ifndef PE_PROBE_GRID_CHUNKS
-#define PE_PROBE_GRID_CHUNKS 0  // timing probe only: cap the round-1 grid chunks (16 B) per env
-#endif
-#ifndef PE_PROBE_VIS_LO
-#define PE_PROBE_VIS_LO 0  // timing probe only: load visit window rows PE_PROBE_VIS_LO..PE_PROBE_VIS_HI only
-#define PE_PROBE_VIS_HI 6
-#endif
-#ifdef PE_ABLATE
-constexpr int kAblate = PE_ABLATE;
-#else
-constexpr int kAblate = 0;
 #endif
 
 // Diagnostic phase stamps (tools/stamps.py builds a SEPARATE library with
@@ -982,41 +962,12 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   uint4 qg1[kGridR1 ? JG1 : 1];
   if constexpr (kGridR1) {
     const uint4* lgq = reinterpret_cast<const uint4*>(st.grid + elc * g.gstride);
-    const int nq = PE_PROBE_GRID_CHUNKS > 0 ? PE_PROBE_GRID_CHUNKS : (int)(g.gstride >> 1);
+    const int nq = (int)(g.gstride >> 1);
 #pragma unroll
     for (int j = 0; j < JG1; ++j) {
       const int q = sub + LT * j;
       qg1[j] = lgq[q < nq ? q : nq - 1];
     }
-  }
-  // timing probe only (PE_PROBE_NOVIS >= 2): PE_PROBE_NOVIS - 1 extra 16-B chunks per
-  // loader thread in round 1 (the cost of a position-independent visit-window cache)
-  constexpr int JX = PE_PROBE_NOVIS >= 2 ? PE_PROBE_NOVIS - 1 : 1;
-  uint4 qx[JX];
-  if constexpr (PE_PROBE_NOVIS >= 2) {
-    const uint4* lxq = reinterpret_cast<const uint4*>(st.vis + elc * g.vstride);
-#pragma unroll
-    for (int j = 0; j < JX; ++j) qx[j] = lxq[sub + LT * j];
-  }
-  constexpr int JV1 = 5;  // G <= 20 visit rows of 16 B (NW == 4)
-  constexpr bool kVisR1 = kGridR1 && PE_VIS_R1;
-  uint4 qv1[kVisR1 ? JV1 : 1];
-  if constexpr (kVisR1) {
-    const uint4* lvq = reinterpret_cast<const uint4*>(st.vis + elc * g.vstride);
-#pragma unroll
-    for (int j = 0; j < JV1; ++j) {
-      const int q = sub + LT * j;
-      qv1[j] = lvq[q < g.G ? q : g.G - 1];
-    }
-  }
-  if constexpr ((kAblate & 64) != 0) {  // diagnostic only: whole-block streaming probe
-    const uint4* gsrc = reinterpret_cast<const uint4*>(st.grid + e0 * g.gstride);
-    const uint4* vsrc = reinterpret_cast<const uint4*>(st.vis + e0 * g.vstride);
-    const int ng = (int)(EPB * g.gstride / 2), nv = (int)(EPB * g.vstride / 4);
-    uint32_t acc = 0;
-    for (int k = threadIdx.x; k < ng; k += blockDim.x) acc ^= gsrc[k].x ^ gsrc[k].w;
-    for (int k = threadIdx.x; k < nv; k += blockDim.x) acc ^= vsrc[k].y ^ vsrc[k].z;
-    reinterpret_cast<uint32_t*>(smem + tile_off)[threadIdx.x] = acc;
   }
   load_tables_hot(smem, st.tab, a.g.G, Rr);
   // the sector rays' tables (pe_quad.hpp quad_rays): dist[R+1] = 1.0, one-hot rows
@@ -1116,7 +1067,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   }
   // ---- round 2: window rows of env le -> LDS [row][env] (loader role)
   uint32_t eo = 0u, en = 0u;
-  if (llive && !(kAblate & 4)) {
+  if (llive) {
     const int lx = (int)(lw.x & 0xFF), ly = (int)((lw.x >> 8) & 0xFF);
     const uint64_t* lgb = st.grid + el * g.gstride;
     const int base = lx - Rr - 1;  // grid row of LDS row 0
@@ -1139,11 +1090,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
         }
       }
       const uint32_t* lvb = st.vis + el * g.vstride;
-      if constexpr (!kVisR1 && !PE_PROBE_NOVIS) {
+      {
 #pragma unroll
         for (int j = 0; j < JV; ++j) {
-          int kk = sub + LT * j;
-          if (PE_PROBE_VIS_LO > 0 || PE_PROBE_VIS_HI < 6) kk = kk < PE_PROBE_VIS_LO ? PE_PROBE_VIS_LO : (kk > PE_PROBE_VIS_HI ? PE_PROBE_VIS_HI : kk);
+          const int kk = sub + LT * j;
           const int xr = lx - 3 + kk;
           const int xc = xr < 0 ? 0 : (xr >= g.G ? g.G - 1 : xr);
           qv[j] = *reinterpret_cast<const uint4*>(lvb + (int64_t)xc * 4);  // g.NW == 4
@@ -1172,7 +1122,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
 #pragma unroll
       for (int j = 0; j < JG; ++j) {
         const int pp = sub + LT * j;
-        if (!kGridR1 && pp < NP && !(kAblate & 32)) {
+        if (!kGridR1 && pp < NP) {
           const int ra = ps + 2 * pp;
           const int rc = ra < 0 ? 0 : (ra > gmax ? gmax : ra);
           const uint64_t lo = (uint64_t)qg[j].x | ((uint64_t)qg[j].y << 32);
@@ -1188,36 +1138,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
       // visit rows: one 16-B row per load, funnel-shifted to ybv
       const int lybv = ly > 0 ? ly - 1 : 0;
       const int vw = (4 * lybv) >> 5, vo = (4 * lybv) & 31;
-      if constexpr (kVisR1) {
-        // the block's rows inside the window, then the off-map rows (visit 10: 1.0)
-#pragma unroll
-        for (int j = 0; j < JV1; ++j) {
-          const int xr = sub + LT * j, k = xr - (lx - 3);
-          if (xr < g.G && k >= 0 && k < NV) {
-            const uint4 q = qv1[j];
-            const uint32_t lo = vw == 0 ? q.x : (vw == 1 ? q.y : q.z);
-            const uint32_t hi = vw == 0 ? q.y : (vw == 1 ? q.z : q.w);
-            lvis[k * LS + le] = vo ? ((lo >> vo) | (hi << (32 - vo))) : lo;
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < JV; ++j) {
-          const int k = sub + LT * j, xr = lx - 3 + k;
-          if (k < NV && (xr < 0 || xr >= g.G)) lvis[k * LS + le] = 0xAAAAAAAAu;
-        }
-      }
 #pragma unroll
       for (int j = 0; j < JV; ++j) {
         const int k = sub + LT * j;
-        if (PE_PROBE_NOVIS && k < NV) {  // timing probe: no visit round
-          uint32_t acc = 0u;
-          if constexpr (PE_PROBE_NOVIS >= 2) {
-#pragma unroll
-            for (int i = 0; i < JX; ++i) acc ^= qx[i].x ^ qx[i].y ^ qx[i].z ^ qx[i].w;
-          }
-          lvis[k * LS + le] = acc == 0x9E3779B9u ? 0x22222222u : 0x11111111u;
-        }
-        if (!kVisR1 && !PE_PROBE_NOVIS && k < NV && !(kAblate & 16)) {
+        if (k < NV) {
           const int xr = lx - 3 + k;
           uint32_t lo = 0xAAAAAAAAu, hi = 0xAAAAAAAAu;  // off-map row: visit 10 (reads 1.0)
           if (xr >= 0 && xr < g.G) {
@@ -1368,7 +1292,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
     const int vs = 4 * (yp - ybv);
     if constexpr (RT) {
       quad_rays_rt<OT>(lrow, st.ldxy, wv * Cr / NW, (wv + 1) * Cr / NW, Rr, lane, kc, sh, watered, row, tdist);
-    } else if constexpr (!(kAblate & 2)) {
+    } else {
       sector_rays<C, R, NW>(wv, lrow, lane, kc, sh, watered, row, tdist);
     }
     // slice rows and position go to the non-commit waves (the commit wave is the laggard)
@@ -1383,7 +1307,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
         row[5 * Cr + 1] = tpos[yp];
       }
     }
-    if (wv == CW && !(kAblate & 8)) {
+    if (wv == CW) {
       // ---- commit (plantos_env.py:160-222)
       uint32_t wo = eo, wn = en;  // explored-bitmap words after the move (bitmap mode)
       if (ok) {
@@ -1513,21 +1437,18 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // stores are still in flight (no fence at the barrier above), and the compiler
   // would make every iteration of its store loop wait for them (s_waitcnt vmcnt(0)
   // before re-using a store's data registers)
-  if constexpr (!(kAblate & 1)) {
-    if constexpr (CM >= 64) {  // long rows: the commit wave's share pays for its wait (64x64: 33.2 -> 32.7 us)
-      if (wv == CW) __builtin_amdgcn_s_waitcnt(0x0F70);  // tracked vmcnt(0): no wait inside the loop
+  if constexpr (CM >= 64) {  // long rows: the commit wave's share pays for its wait (64x64: 33.2 -> 32.7 us)
+    if (wv == CW) __builtin_amdgcn_s_waitcnt(0x0F70);  // tracked vmcnt(0): no wait inside the loop
+    if constexpr (BT)
+      store_tile_codes(rows, ctab, a.obs + e0 * g.D, (int)valid, g.D, (int)threadIdx.x, (int)blockDim.x);
+    else
+      store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D);
+  } else {
+    if (wv != CW) {
       if constexpr (BT)
-        store_tile_codes(rows, ctab, a.obs + e0 * g.D, (int)valid, g.D, (int)threadIdx.x, (int)blockDim.x);
+        store_tile_codes(rows, ctab, a.obs + e0 * g.D, (int)valid, g.D, (int)threadIdx.x, 64 * (NW - 1));
       else
-        store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D);
-    } else {
-      if (wv != CW) {
-        if constexpr (BT) {
-          store_tile_codes(rows, ctab, a.obs + e0 * g.D, (int)valid, g.D, (int)threadIdx.x, 64 * (NW - 1));
-        } else {
-          store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D, (int)threadIdx.x, 64 * (NW - 1));
-        }
-      }
+        store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D, (int)threadIdx.x, 64 * (NW - 1));
     }
   }
   if (any_done && a.autoreset && !quad_coop(a, ndone) && (BT || reset_scratch_bytes(g.G, g.WPR, rl.P) <= 4 * g.D)) {

@@ -25,7 +25,7 @@ def build(ablate=0):
     so = SO if not ablate else SO.replace(".so", f"_abl{ablate}.so")
     sys.path.insert(0, os.path.join(REPO, "rl-env_amd"))
     import build as B
-    B.build(force=True, out=so, extra_flags=["-DPE_STAMPS", "-DPE_DEBUG_KNOBS", f"-DPE_ABLATE={ablate}"],
+    B.build(force=True, out=so, extra_flags=["-DPE_STAMPS", "-DPE_DEBUG_KNOBS"],
             obj_dir=os.path.join(os.path.dirname(so), f"obj{ablate}"))
     print(so)
 
