@@ -299,8 +299,9 @@ def gather_leg(torch, dist, device, shard, Kg, gather_step, world):
             "root_ingress_bytes_per_step": per_rank * (world - 1),
             "root_ingress_GBps": per_rank * (world - 1) / (us * 1e-6) / 1e9,
             "launch": f"{Kg} direct host launches, each step's gather issued async (double-buffered)",
-            "collective": (f"torch.distributed.gather over {backend} to rank 0" if world > 1
-                           else "none: one rank, nothing to gather (the step into the slot buffers only)")}
+            "collective": (f"torch.distributed.gather over {backend} to rank 0" + (" (one rank: to itself)" if world == 1
+                                                                                     else "")
+                           if dist else "none: one rank, nothing to gather (the step into the slot buffers only)")}
 
 
 class _SelftestBatch:
@@ -374,7 +375,10 @@ def main():
     import torch
     dist = None
     nccl_version = None
-    if world > 1:
+    # a process group whenever a launcher started this process (WORLD_SIZE set) -- also
+    # for one rank, so a torchrun job of one runs the same RCCL path (init, barriers,
+    # max-over-ranks, the gather leg) as the 8-GPU job
+    if "WORLD_SIZE" in os.environ:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -384,7 +388,7 @@ def main():
             nccl_version = ".".join(str(v) for v in torch.cuda.nccl.version())
         except Exception:  # noqa: BLE001
             nccl_version = "unknown"
-    device = torch.device("cuda", local if world > 1 else 0)
+    device = torch.device("cuda", local if dist else 0)
     torch.cuda.set_device(device)
 
     from plantos_amd import PlantOSBatch, _capi
@@ -492,7 +496,7 @@ def main():
                          "bytes_per_env_step": B, "kernel_ms": kern_ms},
             "lib_sha": sha,
         }
-        if world > 1:
+        if dist:
             out["config"]["rccl"] = nccl_version
         tr = measured_traffic(out["config"], sha)
         if tr is not None:

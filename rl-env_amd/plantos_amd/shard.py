@@ -30,6 +30,9 @@ class ShardedPlantOS:
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # the collectives run whenever a process group exists -- also with one rank (a
+        # torchrun job of one: the same RCCL code path, gathering to itself)
+        self._coll = dist.is_initialized()
         self.n = int(envs_per_rank)
         lo, _ = shard_range(self.rank, self.world, self.n)
         if batch_factory is None:
@@ -84,7 +87,7 @@ class ShardedPlantOS:
         env order on `root` (None elsewhere): ONE gather of each rank's packed
         output buffer (RCCL over xGMI on GPUs)."""
         flat = self._pack()
-        if self.world == 1:
+        if not self._coll:
             return self.unpack([flat])
         lst = [torch.empty_like(flat) for _ in range(self.world)] if self.rank == root else None
         dist.gather(flat, lst, dst=root, group=self.group)
@@ -105,7 +108,7 @@ class ShardedPlantOS:
         if self._slots is None:
             self._slots = [b.new_io(), b.new_io()]
             self._glist = [[torch.empty_like(self._slots[k]) for _ in range(self.world)]
-                           if (self.rank == root and self.world > 1) else None for k in range(2)]
+                           if (self.rank == root and self._coll) else None for k in range(2)]
             self._work = [None, None]
             self._root = root
             self._k = 0
@@ -116,7 +119,7 @@ class ShardedPlantOS:
             self._work[k] = None
         b.step(actions_local, io=self._slots[k])
         self._last_io = self._slots[k]
-        if self.world > 1:
+        if self._coll:
             self._work[k] = dist.gather(self._slots[k], self._glist[k], dst=root, group=self.group, async_op=True)
         return k
 
@@ -124,7 +127,7 @@ class ShardedPlantOS:
         """Root: the W ranks' packed buffers of slot k (rank order); None elsewhere."""
         if self._slots is None:
             raise ValueError("no step_gather yet")
-        if self.world == 1:
+        if not self._coll:
             return [self._slots[k]]
         return self._glist[k]
 
