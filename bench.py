@@ -192,12 +192,19 @@ def upload_graph(torch, gr):
         return False
 
 
+DIRECT_MAX = 256  # windows of at most this many steps: direct launches (see plan_graph)
+
+
 def plan_graph(K, graph_max, pf):
-    """Steps per captured graph for a K-step window (0: direct launches).  A window of
-    K <= graph_max steps is one K-step graph replayed once; a longer one replays a
-    graph whose length is a multiple of the prefetch cadence pf (every replay then
-    holds the same share of prefetch launches), the rest as direct launches."""
-    if graph_max <= 1 or K <= 1:
+    """Steps per captured graph for a K-step window (0: direct launches).  A short
+    window (K <= DIRECT_MAX, e.g. the driver's 20 steps) is direct launches: the first
+    replay of a freshly captured graph ran ~0.4-2 us per step slower than later ones,
+    and slower than direct launches, whose host cost hides behind the kernels
+    (--steps 20: 10.26-10.35 us per step direct vs 10.5-12.4 graph, alternating runs,
+    profiles/r3p_drv_ab.jsonl).  A longer one replays a graph whose length is a
+    multiple of the prefetch cadence pf (every replay then holds the same share of
+    prefetch launches), the rest as direct launches."""
+    if graph_max <= 1 or K <= DIRECT_MAX:
         return 0
     if K <= graph_max:
         return K

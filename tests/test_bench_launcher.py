@@ -36,17 +36,19 @@ def test_launcher_starts_n_ranks_gloo():
 
 
 def test_graph_plan_and_launch_label():
-    """the driver's short window (--steps 20) is ONE captured 20-step graph, and the
-    line's launch label says what the timed loop executed"""
+    """the driver's short window (--steps 20) is direct launches, long windows replay
+    graphs aligned to the prefetch cadence, and the line's launch label says what the
+    timed loop executed"""
     sys.path.insert(0, REPO)
     import bench
-    assert bench.plan_graph(20, 64, 256) == 20
-    assert bench.launch_label(20, 20) == "hipGraph: 1 replay of 20 captured pe_step launches"
+    assert bench.plan_graph(20, 64, 256) == 0
+    assert bench.launch_label(20, 0) == "20 direct host launches (one pe_step per step)"
     assert bench.plan_graph(153000, 64, 256) == 256
     assert bench.launch_label(1000, 256) == "hipGraph: 3 replays of 256 captured pe_step launches + 232 direct host launches"
+    assert bench.launch_label(20, 20) == "hipGraph: 1 replay of 20 captured pe_step launches"
     assert bench.plan_graph(300, 64, 0) == 64
-    assert bench.plan_graph(100, 0, 256) == 0
-    assert bench.launch_label(5, 0) == "5 direct host launches (one pe_step per step)"
+    assert bench.plan_graph(300, 512, 256) == 300
+    assert bench.plan_graph(100000, 0, 256) == 0
 
 
 def test_too_few_gpus_is_an_error():
