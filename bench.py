@@ -154,9 +154,11 @@ def lib_sha(path):
 def measured_traffic(cfg, sha):
     """Per-launch HBM bytes of this kernel/config from the committed rocprofv3 PMC
     summaries (profiles/pmc*_*.json, tools/pmc_summary.py), ONLY from a profile of
-    this exact library (lib_sha of the .so the bench loaded).  traffic = 2 x
-    FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts half the bytes of wide
-    coalesced reads, MI355X_MICROARCH.md §HBM); the raw sum is kept beside it."""
+    this exact library (lib_sha of the .so the bench loaded).  traffic = FETCH_SIZE
+    + WRITE_SIZE with the gfx950 x2 applied to the kernel's streamed reads only
+    (MI355X_MICROARCH.md §HBM; calibrated on known byte counts of our access shapes,
+    profiles/r3r_fetch_calibration.json: gathered 16-B rows are counted in full);
+    the raw sum and the all-reads-x2 upper bound are kept beside it."""
     import glob
     best = None
     for p in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc*_*.json"))):
@@ -171,7 +173,9 @@ def measured_traffic(cfg, sha):
     if best is None:
         return None
     p, d = best
-    return {"traffic": d["traffic_hi"], "traffic_raw": d["traffic"], "source": os.path.relpath(p, REPO)}
+    return {"traffic": d.get("traffic_cal", d["traffic_hi"]), "traffic_raw": d["traffic"],
+            "traffic_hi": d["traffic_hi"], "source": os.path.relpath(p, REPO),
+            "calibration": d.get("calibration")}
 
 
 # ---------------------------------------------------------------- timed windows
@@ -508,7 +512,9 @@ def main():
         tr = measured_traffic(out["config"], sha)
         if tr is not None:
             out["roofline"].update({"traffic": tr["traffic"], "traffic_raw": tr["traffic_raw"],
-                                    "traffic_source": tr["source"], "traffic_per_env_step": tr["traffic"] / n})
+                                    "traffic_all_reads_x2": tr["traffic_hi"], "traffic_source": tr["source"],
+                                    "traffic_calibration": tr["calibration"],
+                                    "traffic_per_env_step": tr["traffic"] / n})
         else:
             out["roofline"]["traffic_note"] = f"no committed PMC profile of this library (lib_sha {sha})"
         if desync is not None:

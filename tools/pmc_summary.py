@@ -15,8 +15,15 @@ dominant kernel:
                          wide coalesced streaming read; upper bound for our mix of
                          16-B coalesced and 4/8-B gathered loads)
   traffic             = fetch_bytes_raw + write_bytes (raw counters);
-  traffic_hi          = fetch_bytes_x2 + write_bytes: the corrected figure bench.py reports as
-                        roofline.traffic (for a profile whose lib_sha is the benched library's).
+  traffic_hi          = fetch_bytes_x2 + write_bytes: every read treated as streamed (upper bound);
+  traffic_cal         = fetch_bytes_raw + streamed/2 + write_bytes: the calibrated figure bench.py
+                        reports as roofline.traffic (for a profile whose lib_sha is the benched
+                        library's).  profiles/r3r_fetch_calibration.json measured FETCH_SIZE on
+                        known byte counts: streamed 16-B / 4-B reads report 1/2 of their bytes,
+                        random 64-B segments and 16-B / 8-B gathers their full request bytes --
+                        so only the kernel's streamed reads (--streamed-bytes per env: the sector
+                        kernels' packed scalars 16 B + int32 action 4 B + return 8 B = 28 B) need
+                        the x2, the gathered rows are counted as they are.
 """
 import argparse
 import collections
@@ -58,6 +65,8 @@ def main():
     ap.add_argument("--bench-json", default=None, help="bench line of the profiled run (config)")
     ap.add_argument("--fetch-dir", default=None, help="FETCH_SIZE pass dir under gpurun_out (tools/gpu_session.sh: pmcf_TAG)")
     ap.add_argument("--write-dir", default=None, help="WRITE_SIZE pass dir under gpurun_out (tools/gpu_session.sh: pmcw_TAG)")
+    ap.add_argument("--streamed-bytes", type=float, default=28.0,
+                    help="streamed (coalesced, 16-B / 4-B per lane) read bytes per env-step of the kernel")
     a = ap.parse_args()
     g = os.path.join(REPO, "gpurun_out")
     fd = a.fetch_dir or f"{a.prefix}_fetch_{a.tag}"
@@ -77,7 +86,7 @@ def main():
         "fetch_bytes_raw": f_kib * 1024, "fetch_bytes_x2": 2 * f_kib * 1024, "write_bytes": w_kib * 1024,
         "traffic": (f_kib + w_kib) * 1024, "traffic_hi": (2 * f_kib + w_kib) * 1024,
         "resources": meta[k],
-        "calibration": {n: statistics.mean(write[n]) for n in write if "synth" in n},
+        "write_calibration": {n: statistics.mean(write[n]) for n in write if "synth" in n},
         "method": "rocprofv3 --pmc FETCH_SIZE --kernel-trace, then --pmc WRITE_SIZE --kernel-trace (separate passes)",
     }
     if a.bench_json:
@@ -89,6 +98,10 @@ def main():
             out["lib_sha"] = b.get("lib_sha")  # bench.py cites this profile only for this exact library
             out["traffic_per_env_step"] = out["traffic"] / n
             out["traffic_hi_per_env_step"] = out["traffic_hi"] / n
+            out["streamed_read_bytes_per_env_step"] = a.streamed_bytes
+            out["traffic_cal"] = out["traffic"] + a.streamed_bytes * n / 2
+            out["traffic_cal_per_env_step"] = out["traffic_cal"] / n
+            out["calibration"] = "profiles/r3r_fetch_calibration.json"
         except (OSError, IndexError, KeyError, ValueError):
             pass
     sd = a.stats_dir
