@@ -89,7 +89,10 @@ struct State {
   const Tables* tab;
   const signed char* ldx;  // [C][R] LIDAR offsets (generic kernel)
   const signed char* ldy;
-  const int16_t* ldxy;     // [C][(R+7)&~7] (dx & 0xFF) | dy << 8, zero-padded (pe_step_wave's LDS header)
+  // [C][(R+7)&~7] (dx & 0xFF) | dy << 8, zero-padded (pe_step_wave's LDS header, the
+  // runtime sector kernel's probes); for pe_step_wave<., true> the same probes as
+  // [C][RP] u16 aligned-window byte offsets, then [C][RP] u8 bit shifts (pe_create)
+  const int16_t* ldxy;
   uint32_t* err_bits;      // OR of error flags raised since the last poll
   CurRec* cur;             // batched CurriculumWrapper records, NULL when disabled
 };

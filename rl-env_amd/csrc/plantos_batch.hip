@@ -501,6 +501,12 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
 #ifndef PE_GRID_R1
 #define PE_GRID_R1 1  // one-word sector kernel: the grid block in round 1 (A/B: -DPE_GRID_R1=0)
 #endif
+#ifndef PE_WAVE_ROWSTORE_MIN
+// pe_step_wave's obs row of D >= this many floats as 16-B stores (shorter: one float per
+// lane): 64x64/C64/R32 93.8 -> 90.4 us, 40x40/C48/R8 76.7 -> 75.0, but 8x8/C16/R20
+// 68.0 -> 70.2 (sc1 16-B stores: 90.8 / 76.7 / 70.4; profiles/r3x/)
+#define PE_WAVE_ROWSTORE_MIN 200
+#endif
 #ifndef PE_STAGGER_GROUPS
 #define PE_STAGGER_GROUPS 4  // sector kernel: the grid's start-delay groups (A/B: -DPE_STAGGER_GROUPS=n)
 #endif
@@ -1491,7 +1497,11 @@ __host__ __device__ constexpr int wave_lds_floats(int G, int R, int WPR, int NW,
 // The workgroup's shared header: the obs tables (Tables' first 344 floats: dist,
 // pos, vis) and the LIDAR offsets as int16 (dx & 0xFF | dy << 8) [C][RP], RP = R
 // rounded up to 8 (one 16-B LDS read per 8 probes of a ray).
-__host__ __device__ constexpr int wave_hdr_floats(int C, int R) { return 344 + C * ((R + 7) & ~7) / 2; }
+// (the rover-aligned kernels' entries are 3 B: a u16 LDS byte offset [C][RP], then a u8
+// bit shift [C][RP]; rounded up to 16 B)
+__host__ __device__ constexpr int wave_hdr_floats(int C, int R, bool aln) {
+  return 344 + (aln ? ((C * ((R + 7) & ~7) * 3 + 15) & ~15) / 4 : C * ((R + 7) & ~7) / 2);
+}
 constexpr int kWaveEnvs = 8;  // envs (waves) per workgroup
 // Rover-aligned window (ALN): after the transition the post-move rows xp-R .. xp+R
 // are re-staged over the raw window, each shifted so that cell yp+dy+R of the
@@ -1506,13 +1516,10 @@ __host__ __device__ constexpr bool wave_aln_ok(int G, int R, int WPR) {
   return wave_aln_words(R) <= 64 * kAlnSlots && wave_aln_words(R) <= 2 * wave_win_words(G, R, WPR);
 }
 // one packed (dx & 0xFF | dy << 8) offset -> the aligned window's (word | shift << 11)
-__device__ __forceinline__ uint32_t aln_entry(uint32_t v, int R, int NWA) {
+__host__ __device__ __forceinline__ uint32_t aln_entry(uint32_t v, int R, int NWA) {
   const int dx = (int)(int8_t)(v & 0xFFu), dy = (int)(int8_t)((v >> 8) & 0xFFu);
   const int cb = 2 * (dy + R);
   return (uint32_t)((dx + R) * NWA + (cb >> 5)) | ((uint32_t)(cb & 31) << 11);
-}
-__device__ __forceinline__ uint32_t aln_pair(uint32_t w, int R, int NWA) {
-  return aln_entry(w & 0xFFFFu, R, NWA) | (aln_entry(w >> 16, R, NWA) << 16);
 }
 
 // The wave kernel's done path (terminal obs / info, auto-reset), called by the
@@ -1584,24 +1591,19 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
   const float* tsrc = reinterpret_cast<const float*>(tab);
   for (int k = threadIdx.x; k < 344; k += blockDim.x) smem[k] = tsrc[k];
   int16_t* lofs = reinterpret_cast<int16_t*>(smem + 344);
-  {  // the packed offsets, 16 B per thread and pass (st.ldxy, built by pe_create)
+  {  // the probe table, 16 B per thread and pass (st.ldxy, built by pe_create -- the
+     // aligned-window entries too: converted here they cost 135 VALU per pass)
     const uint4* src = reinterpret_cast<const uint4*>(st.ldxy);
     uint4* dst = reinterpret_cast<uint4*>(lofs);
-    for (int k = threadIdx.x; k < g.C * RP / 8; k += blockDim.x) {
-      uint4 v = src[k];
-      if constexpr (ALN) {
-        const int NWA = (4 * R + 33) >> 5;
-        v = make_uint4(aln_pair(v.x, R, NWA), aln_pair(v.y, R, NWA), aln_pair(v.z, R, NWA), aln_pair(v.w, R, NWA));
-      }
-      dst[k] = v;
-    }
+    const int nq = ALN ? (g.C * RP * 3 + 15) >> 4 : g.C * RP / 8;
+    for (int k = threadIdx.x; k < nq; k += blockDim.x) dst[k] = src[k];
   }
   __syncthreads();
   if (e >= a.n) return;  // wave-uniform; no workgroup barrier below
   const float* tdist = smem;
   const float* tpos = smem + 72;
   const float* tvis = smem + 328;
-  float* base = smem + wave_hdr_floats(g.C, R) + wv * wave_lds_floats(G, R, WPR, NW, D);
+  float* base = smem + wave_hdr_floats(g.C, R, ALN) + wv * wave_lds_floats(G, R, WPR, NW, D);
   uint64_t* win = reinterpret_cast<uint64_t*>(base);
   uint32_t* lvis = reinterpret_cast<uint32_t*>(base + 2 * wave_win_words(G, R, WPR));
   float* row = base + 2 * wave_win_words(G, R, WPR) + ((7 * NW + 3) & ~3);
@@ -1821,12 +1823,17 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
+  const char* wbyte = reinterpret_cast<const char*>(win);
   for (int i = lane; i < g.C; i += 64) {
     const uint4* orow = reinterpret_cast<const uint4*>(lofs + i * RP);
+    const uint2* srow = reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(lofs) + g.C * RP * 2 + i * RP);
     int dist = R, ent = EMPTY;
     for (int r0 = 0; r0 < R; r0 += 8) {  // 8 probes per 16-B offset read, their codes in flight together
       const uint4 o = orow[r0 >> 3];
       const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+      uint2 os = make_uint2(0u, 0u);
+      if constexpr (ALN) os = srow[r0 >> 3];
+      const uint32_t sw[2] = {os.x, os.y};
       // the 8 probe codes packed 2 bits each (probe j at bits 2j), first hit by one
       // find-first-set (as the sector kernel's quad_rays); 32-bit window reads (a
       // 2-bit code never straddles a word: its bit offset is even; the row offset as a
@@ -1836,8 +1843,10 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
       for (int j = 0; j < 8; ++j) {
         const uint32_t v = ow[j >> 1] >> (16 * (j & 1));
         uint32_t c;
-        if constexpr (ALN) {  // table word and shift; off-map rows hold OBST
-          c = (win32[v & 0x7FFu] >> ((v >> 11) & 31u)) & 3u;
+        if constexpr (ALN) {  // the probe's LDS byte offset and bit shift; off-map rows hold OBST
+          // (ubfe reads the low 5 bits of its offset operand: the shift byte needs no mask)
+          c = __builtin_amdgcn_ubfe(*reinterpret_cast<const uint32_t*>(wbyte + (v & 0xFFFFu)),
+                                    sw[j >> 2] >> (8 * (j & 3)), 2u);
         } else {
           const int cx = xp + (int)(int8_t)(v & 0xFFu);
           const int bit = 2 * (yp + (int)(int8_t)((v >> 8) & 0xFFu) + R);
@@ -1879,8 +1888,25 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
     const StepArgs* ap = (const StepArgs*)__builtin_amdgcn_kernarg_segment_ptr();
     wave_done<MAXW>(*ap, e, s, wfix, row, win, tdist, tpos, tvis, lane);
   }
+  // the obs row: long rows as 16-B stores from the first 16-B boundary of the row on,
+  // the 0-3 floats before it and the tail as single floats
   float* dst = a.obs + e * D;
-  for (int k = lane; k < D; k += 64) dst[k] = row[k];
+  const int hd = (int)((16u - ((uint32_t)reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u) >> 2;
+  const int n4 = (D - hd) >> 2;
+  // (rover-aligned kernels only: in the other one its registers made the SGPRs spill, and
+  // none of its geometries benched has rows that long)
+  if (ALN && D >= PE_WAVE_ROWSTORE_MIN && (reinterpret_cast<uintptr_t>(dst) & 3u) == 0) {
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    for (int k = lane; k < n4; k += 64) {
+      const float* sr = row + hd + 4 * k;
+      const v4f v = {sr[0], sr[1], sr[2], sr[3]};
+      *reinterpret_cast<v4f*>(dst + hd + 4 * k) = v;
+    }
+    if (lane < hd) dst[lane] = row[lane];
+    if (lane < D - hd - 4 * n4) dst[hd + 4 * n4 + lane] = row[hd + 4 * n4 + lane];
+  } else {
+    for (int k = lane; k < D; k += 64) dst[k] = row[k];
+  }
 }
 
 // reset() with one wave per env (pe_coop.hpp): the map, grid/visit rows and the
@@ -2374,7 +2400,7 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
       case V_C64R6: hipLaunchKernelGGL((pe_step_fast<64, 6, false>), grid, block, lds, s, a); break;
       default: {  // pe_step_wave: one wave per env
         const Geo& g = h->g;
-        const size_t wlds = sizeof(float) * ((size_t)wave_hdr_floats(g.C, g.R) +
+        const size_t wlds = sizeof(float) * ((size_t)wave_hdr_floats(g.C, g.R, wave_aln_ok(g.G, g.R, g.WPR)) +
                                              kWaveEnvs * (size_t)wave_lds_floats(g.G, g.R, g.WPR, g.NW, g.D));
         dim3 wgrid((unsigned)((h->n + kWaveEnvs - 1) / kWaveEnvs)), wblock(64 * kWaveEnvs);
         const bool aln = wave_aln_ok(g.G, g.R, g.WPR);
@@ -2576,7 +2602,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
     delete h;
     return fail(PE_ERR_ARG, "observation tile does not fit LDS (lidar_channels <= 120)");
   }
-  if (sizeof(float) * ((size_t)wave_hdr_floats(C, R) + kWaveEnvs * (size_t)wave_lds_floats(G, R, g.WPR, g.NW, g.D)) >
+  if (sizeof(float) * ((size_t)wave_hdr_floats(C, R, wave_aln_ok(G, R, g.WPR)) + kWaveEnvs * (size_t)wave_lds_floats(G, R, g.WPR, g.NW, g.D)) >
       160 * 1024) {
     delete h;
     return fail(PE_ERR_ARG, "the one-wave-per-env step kernel's window does not fit LDS");
@@ -2738,7 +2764,8 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   const size_t o_tab = carve(sizeof(Tables));
   const size_t o_ldx = carve(nl), o_ldy = carve(nl);
   const int RP = (R + 7) & ~7;
-  const size_t o_ldxy = carve((size_t)C * RP * 2);
+  const bool wave_aln = h->variant == V_GENERIC && wave_aln_ok(G, R, g.WPR);  // pe_step_wave<., true>
+  const size_t o_ldxy = carve(wave_aln ? ((size_t)C * RP * 3 + 15) & ~(size_t)15 : (size_t)C * RP * 2);
   const size_t o_err = carve(sizeof(uint32_t));
   const size_t o_scal = carve(n * sizeof(uint4));
   const size_t o_ret = carve(n * sizeof(double));
@@ -2810,7 +2837,20 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   for (int i = 0; i < C; ++i)
     for (int r = 0; r < R; ++r)
       ldxy[(size_t)i * RP + r] = (int16_t)((uint8_t)ldx[i * R + r] | ((int)ldy[i * R + r] << 8));
-  hipError_t e5 = hipMemcpy(base + o_ldxy, ldxy.data(), ldxy.size() * 2, hipMemcpyHostToDevice);
+  hipError_t e5;
+  if (wave_aln) {  // pe_step_wave<., true>'s LDS header entries: [C][RP] u16 byte offsets into
+                   // the aligned window, then [C][RP] u8 bit shifts
+    std::vector<uint8_t> aln(((ldxy.size() * 3 + 15) & ~(size_t)15), 0);
+    for (size_t k = 0; k < ldxy.size(); ++k) {
+      const uint32_t en = aln_entry((uint16_t)ldxy[k], R, (4 * R + 33) >> 5);
+      const uint16_t off = (uint16_t)(4u * (en & 0x7FFu));
+      std::memcpy(aln.data() + 2 * k, &off, 2);
+      aln[2 * ldxy.size() + k] = (uint8_t)((en >> 11) & 31u);
+    }
+    e5 = hipMemcpy(base + o_ldxy, aln.data(), aln.size(), hipMemcpyHostToDevice);
+  } else {
+    e5 = hipMemcpy(base + o_ldxy, ldxy.data(), ldxy.size() * 2, hipMemcpyHostToDevice);
+  }
   delete[] ldx;
   delete[] ldy;
   if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess || e5 != hipSuccess) {
