@@ -1587,7 +1587,18 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int64_t e = (int64_t)blockIdx.x * kWaveEnvs + wv;
   const int G = g.G, R = g.R, WPR = g.WPR, NW = g.NW, D = g.D, RP = (R + 7) & ~7;
-  // the shared header (its loads overlap round 1 below; read after the barrier)
+  // ---- round 1 (uniform): the packed scalars and both action words in one round
+  // trip, issued before the shared header's copy (a wave's round 1 waited for the
+  // header's loads and the barrier before it started) -- unconditional loads at an
+  // index clamped into the batch (the action's load inside a branch on act_bytes
+  // was waited for before the return's was issued: three round trips before round 2)
+  const int64_t ec = e < a.n ? e : (int64_t)a.n - 1;
+  const uint4 sw = st.scal[ec];
+  const int ash = a.act_bytes == 8 ? 1 : 0;  // 8-byte actions: two words, low first
+  const int32_t* ap = reinterpret_cast<const int32_t*>(a.actions);
+  const int32_t alo = ap[ec << ash], ahi = ap[(ec << ash) + ash];
+  double ret = st.ep_ret[ec];  // (needed at the commit: in flight through round 2)
+  // the shared header (read after the barrier)
   const float* tsrc = reinterpret_cast<const float*>(tab);
   for (int k = threadIdx.x; k < 344; k += blockDim.x) smem[k] = tsrc[k];
   int16_t* lofs = reinterpret_cast<int16_t*>(smem + 344);
@@ -1608,11 +1619,8 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
   uint32_t* lvis = reinterpret_cast<uint32_t*>(base + 2 * wave_win_words(G, R, WPR));
   float* row = base + 2 * wave_win_words(G, R, WPR) + ((7 * NW + 3) & ~3);
 
-  // ---- round 1 (uniform: scalar loads)
-  Scal s = unpack(st.scal[e]);
-  const int64_t action = a.act_bytes == 8 ? reinterpret_cast<const int64_t*>(a.actions)[e]
-                                          : (int64_t)reinterpret_cast<const int32_t*>(a.actions)[e];
-  double ret = st.ep_ret[e];
+  Scal s = unpack(sw);
+  const int64_t action = ash ? (int64_t)(((uint64_t)(uint32_t)ahi << 32) | (uint32_t)alo) : (int64_t)alo;
   bool mv = false, water = false, bad = false;
   int dxm = 0, dym = 0;
   if (action < 4) {                                        // plantos_env.py:166
@@ -1652,7 +1660,27 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
     const int k = lane + 64 * j;
     vv[j] = vsrc[k < nv ? k : nv - 1];
   }
-  for (int q0 = 0; q0 < nq; q0 += 4 * 64) {  // one pass at G+2R <= 128 cells and 2R+3 rows <= 128
+  {  // the window's first 256 16-B units (all of it up to 2R+3 rows of 4 words, e.g. 64x64/R32)
+    uint4 gv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = lane + 64 * j;
+      gv[j] = gsrc[q < nq ? q : nq - 1];
+    }
+    // every load of round 2 lands here, in one wait (asm operands): as a loop, or with
+    // the loads left to the compiler, some were sunk into the conditional LDS writes
+    // below and each waited for alone (64x64/R32: the visit rows, then 3 window loads)
+    asm volatile("" ::"v"(vv[0]), "v"(vv[1]), "v"(gv[0].x), "v"(gv[1].x), "v"(gv[2].x), "v"(gv[3].x));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = lane + 64 * j;
+      if (q < nq) {
+        win[2 * q] = (uint64_t)gv[j].x | ((uint64_t)gv[j].y << 32);
+        win[2 * q + 1] = (uint64_t)gv[j].z | ((uint64_t)gv[j].w << 32);
+      }
+    }
+  }
+  for (int q0 = 4 * 64; q0 < nq; q0 += 4 * 64) {  // (G+2R > 128 cells with many rows)
     uint4 gv[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -1805,6 +1833,7 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
     uint32_t av[kAlnSlots];
 #pragma unroll
     for (int t = 0; t < kAlnSlots; ++t) {
+      if (64 * t >= tot) break;  // (uniform: slots past the window)
       const int k = lane + 64 * t;
       const int i = NWA == 1 ? k : (int)__umulhi((uint32_t)k, mg), w = k - i * NWA;
       const int xr = xp - R + i;
@@ -1827,7 +1856,10 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
   for (int i = lane; i < g.C; i += 64) {
     const uint4* orow = reinterpret_cast<const uint4*>(lofs + i * RP);
     const uint2* srow = reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(lofs) + g.C * RP * 2 + i * RP);
-    int dist = R, ent = EMPTY;
+    // every round runs (a wave-uniform trip count: no exec-mask bookkeeping per round --
+    // the wave ran all of them anyway unless all 64 rays had hit); the first hit is
+    // kept as (dist << 2 | ent) + 1
+    uint32_t hit = 0u;
     for (int r0 = 0; r0 < R; r0 += 8) {  // 8 probes per 16-B offset read, their codes in flight together
       const uint4 o = orow[r0 >> 3];
       const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
@@ -1858,13 +1890,11 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
       }
       if (R - r0 < 8) pk &= (1u << (2 * (R - r0))) - 1u;  // the zero-padded offsets past R
       const uint32_t nz = (pk | (pk >> 1)) & 0x5555u;
-      if (nz) {
-        const int f = __builtin_ctz(nz);  // 2j of the first hit
-        dist = r0 + (f >> 1) + 1;
-        ent = (int)((pk >> f) & 3u);
-        break;
-      }
+      const int f = __builtin_ctz(nz | 0x10000u);  // 2j of the round's first hit (16: none)
+      const uint32_t cand = nz ? ((uint32_t)(r0 + (f >> 1) + 1) << 2 | ((pk >> f) & 3u)) + 1u : 0u;
+      hit = hit ? hit : cand;
     }
+    const int dist = hit ? (int)((hit - 1u) >> 2) : R, ent = hit ? (int)((hit - 1u) & 3u) : EMPTY;
     row[5 * i] = tdist[dist];                                    // :288
     row[5 * i + 1] = ent == 0 ? 1.0f : 0.0f;
     row[5 * i + 2] = ent == 1 ? 1.0f : 0.0f;
