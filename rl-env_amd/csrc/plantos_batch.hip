@@ -1833,7 +1833,6 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
     uint32_t av[kAlnSlots];
 #pragma unroll
     for (int t = 0; t < kAlnSlots; ++t) {
-      if (64 * t >= tot) break;  // (uniform: slots past the window)
       const int k = lane + 64 * t;
       const int i = NWA == 1 ? k : (int)__umulhi((uint32_t)k, mg), w = k - i * NWA;
       const int xr = xp - R + i;
@@ -1856,10 +1855,7 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
   for (int i = lane; i < g.C; i += 64) {
     const uint4* orow = reinterpret_cast<const uint4*>(lofs + i * RP);
     const uint2* srow = reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(lofs) + g.C * RP * 2 + i * RP);
-    // every round runs (a wave-uniform trip count: no exec-mask bookkeeping per round --
-    // the wave ran all of them anyway unless all 64 rays had hit); the first hit is
-    // kept as (dist << 2 | ent) + 1
-    uint32_t hit = 0u;
+    int dist = R, ent = EMPTY;
     for (int r0 = 0; r0 < R; r0 += 8) {  // 8 probes per 16-B offset read, their codes in flight together
       const uint4 o = orow[r0 >> 3];
       const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
@@ -1890,11 +1886,13 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
       }
       if (R - r0 < 8) pk &= (1u << (2 * (R - r0))) - 1u;  // the zero-padded offsets past R
       const uint32_t nz = (pk | (pk >> 1)) & 0x5555u;
-      const int f = __builtin_ctz(nz | 0x10000u);  // 2j of the round's first hit (16: none)
-      const uint32_t cand = nz ? ((uint32_t)(r0 + (f >> 1) + 1) << 2 | ((pk >> f) & 3u)) + 1u : 0u;
-      hit = hit ? hit : cand;
+      if (nz) {
+        const int f = __builtin_ctz(nz);  // 2j of the first hit
+        dist = r0 + (f >> 1) + 1;
+        ent = (int)((pk >> f) & 3u);
+        break;
+      }
     }
-    const int dist = hit ? (int)((hit - 1u) >> 2) : R, ent = hit ? (int)((hit - 1u) & 3u) : EMPTY;
     row[5 * i] = tdist[dist];                                    // :288
     row[5 * i + 1] = ent == 0 ? 1.0f : 0.0f;
     row[5 * i + 2] = ent == 1 ? 1.0f : 0.0f;

@@ -292,9 +292,12 @@ def test_determinism_and_sharding_equivalence():
         x.close()
 
 
+@pytest.mark.parametrize("name", ["g20", "g16c40", "g8r20"])
 @pytest.mark.parametrize("n", [1, 63, 65, 1000])
-def test_ragged_batch_sizes(n):
-    cfg = CFG["g20"]
+def test_ragged_batch_sizes(n, name):
+    """int64 actions (8-byte action words) and partial workgroups, through the sector
+    kernel and both ray paths of the one-wave-per-env kernel"""
+    cfg = CFG[name]
     b = make(cfg, n, seed=3)
     ov = OracleVec(cfg, np.arange(n), 3)
     for t in range(30):
@@ -305,10 +308,12 @@ def test_ragged_batch_sizes(n):
     b.close()
 
 
-def test_out_of_range_actions():
+@pytest.mark.parametrize("name", ["g20", "g16c40"])
+def test_out_of_range_actions(name):
     """Negative actions wrap like Python list indices (plantos_env.py:187); < -4 is the
-    reference's IndexError, flagged (bit1); >= 4 waters (plantos_env.py:168-169)."""
-    cfg = CFG["g20"]
+    reference's IndexError, flagged (bit1); >= 4 waters (plantos_env.py:168-169) -- in
+    the sector kernel and the one-wave-per-env kernel (int64 actions)."""
+    cfg = CFG[name]
     n = 64
     b = make(cfg, n, seed=4, autoreset=False)
     ov = OracleVec(cfg, np.arange(n), 4)

@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# round-3 GPU session aj: the measurement pass of the product library after this
+# round-3 GPU session aj (run by session_r3ai.sh): the measurement pass of the product library after this
 # session's pe_step_wave changes (the sector kernels' code is unchanged): the GPU suite,
 # smoke, bench lines of every geometry, rocprof kernel stats and FETCH / WRITE PMC passes
 set -euo pipefail
