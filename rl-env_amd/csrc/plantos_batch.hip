@@ -899,7 +899,9 @@ __device__ __forceinline__ void quad_done_obs(const void* ka, int tile_off, int 
 // EPB: envs per workgroup (64; 16 / 32 for small batches: more workgroups, so that
 // a batch of a few thousand envs spreads over every CU -- lanes >= EPB idle).  The
 // LDS layout keeps the 64-env stride LS whatever EPB.
-template <int C, int R, bool ONEWORD, int NW, bool BT = false, int EPB = kQuadEnvs>
+// W2: multi-word rows of exactly 2 words (G + 2R <= 64, e.g. the training scripts' 25x25
+// with R = 6), known at compile time (see round 2's row loads).
+template <int C, int R, bool ONEWORD, int NW, bool BT = false, int EPB = kQuadEnvs, bool W2 = false>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs (small-batch EPB: one workgroup per CU, no cap); NW=4: <= 128 VGPRs (4 workgroups per CU: G=25 13.1 -> 10.5 us; 1-word C16: 122 -> 104 VGPRs)
   // C == 0 (R == 0): the runtime-(C, R) sector kernel (quad_rays_rt): C, R from the
   // geometry (up to kRtCMax / kRtRMax), the LDS layout sized at run time
@@ -1165,7 +1167,21 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
       constexpr int JG = (NR + LT - 1) / LT, JV = (NV + LT - 1) / LT;
       uint64_t glo[JG], ghi[JG];
       uint32_t vlo[JV], vhi[JV];
-      if (g.WPR == 2) {  // (G <= 52, e.g. the training scripts' 25x25) a row is one aligned 16-B load
+      if constexpr (W2) {
+        // a row is one aligned 16-B load, both words kept as loaded: the select of the
+        // window's first word (below, in the LDS write) waits for the load -- done here,
+        // it held the visit-row loads back (two round trips; 25x25 10.42 us); and with a
+        // runtime test of the row width, hipcc merged this path with the general one as
+        // two 8-B loads per row
+#pragma unroll
+        for (int j = 0; j < JG; ++j) {
+          const int xr = base + sub + LT * j;
+          const int xc = xr < 0 ? 0 : (xr >= g.G ? g.G - 1 : xr);
+          const uint4 q = *reinterpret_cast<const uint4*>(lgb + (int64_t)xc * 2);
+          glo[j] = (uint64_t)q.x | ((uint64_t)q.y << 32);
+          ghi[j] = (uint64_t)q.z | ((uint64_t)q.w << 32);
+        }
+      } else if (g.WPR == 2) {  // (G <= 52, e.g. the training scripts' 25x25) a row is one aligned 16-B load
 #pragma unroll
         for (int j = 0; j < JG; ++j) {
           const int xr = base + sub + LT * j;
@@ -1203,8 +1219,9 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
           const int xr = base + k;
           uint64_t v = kEven64;  // off-map rows read as obstacles
           if (xr >= 0 && xr < g.G) {
-            const uint64_t hi = w0 + 1 < g.WPR ? ghi[j] : 0ull;
-            v = o ? ((glo[j] >> o) | (hi << (64 - o))) : glo[j];
+            const uint64_t lo = W2 && w0 ? ghi[j] : glo[j];
+            const uint64_t hi = (W2 ? w0 == 0 : w0 + 1 < g.WPR) ? ghi[j] : 0ull;
+            v = o ? ((lo >> o) | (hi << (64 - o))) : lo;
           }
           lrow[k * LS + le] = v;
         }
@@ -1833,6 +1850,7 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
     uint32_t av[kAlnSlots];
 #pragma unroll
     for (int t = 0; t < kAlnSlots; ++t) {
+      if (64 * t >= tot) break;  // (uniform: slots past the window -- 40x40/R8 uses 1 of 8)
       const int k = lane + 64 * t;
       const int i = NWA == 1 ? k : (int)__umulhi((uint32_t)k, mg), w = k - i * NWA;
       const int xr = xp - R + i;
@@ -2408,7 +2426,12 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
         else
           PE_QUAD(16, 6, true);
         break;
-      case V_QUAD_C16R6: PE_QUAD4(16, 6, false); break;
+      case V_QUAD_C16R6:  // rows of 2 words (G <= 52): the compile-time 2-word row loads
+        if (h->g.WPR == 2)
+          hipLaunchKernelGGL((pe_step_quad<16, 6, false, 4, false, kQuadEnvs, true>), grid, block, lds, s, a);
+        else
+          PE_QUAD4(16, 6, false);
+        break;
       case V_QUAD_C64R6: PE_QUAD(64, 6, false); break;
       case V_QUAD_C10R2_1W: PE_QUAD4(10, 2, true); break;
       case V_QUAD_C10R2: PE_QUAD4(10, 2, false); break;

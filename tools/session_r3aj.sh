@@ -4,7 +4,7 @@
 # smoke, bench lines of every geometry, rocprof kernel stats and FETCH / WRITE PMC passes
 set -euo pipefail
 OUT=gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
-T=r3aj
+T=${PASS_TAG:-r3aj}
 bash tools/gpu_session.sh $T tests
 tail -n 1 $OUT/tests_$T.log
 bash tools/gpu_session.sh $T smoke bench benchx:drv:--steps_20_--warmup_5 bench64 \
