@@ -2,7 +2,7 @@
 # round-3 GPU session ai: the measurement pass of the in-tree product library (w2's
 # pe_step_wave round trips; the sector kernels' code is unchanged): the GPU suite, smoke,
 # bench lines, rocprof kernel stats, FETCH / WRITE PMC passes (tools/session_r3aj.sh) --
-# then a pe_step_wave A/B: HEAD~1 (base), w2 (= the product's source), w6 = w2 + ray
+# then a pe_step_wave A/B: aa1feb1 (base: the session-start source), w2 (= the product's source), w6 = w2 + ray
 # rounds without the per-round early exit, w7 = w6 + re-staging slots past the window
 # skipped (diff profiles/r3ai/uniform_ray_rounds_and_slot_skip.diff)
 set -euo pipefail
