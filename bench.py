@@ -185,10 +185,15 @@ def upload_graph(torch, gr):
     (profiles/r3g_window_first_replay.json).  Best effort: a runtime without it
     just uploads at the first replay."""
     import ctypes
-    import glob
     try:
-        lib = glob.glob(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so*"))
-        hip = ctypes.CDLL(lib[0] if lib else "libamdhip64.so")
+        # the HIP runtime this process already has mapped (the one torch loaded): a
+        # runtime opened by name could be another copy, whose hipGraphUpload would get a
+        # graph-exec handle it does not own
+        with open("/proc/self/maps") as f:
+            paths = {ln.split()[-1] for ln in f if "libamdhip64.so" in ln and ln.split()[-1].startswith("/")}
+        if len(paths) != 1:
+            return False
+        hip = ctypes.CDLL(paths.pop())
         exe = gr.raw_cuda_graph_exec()
         hip.hipGraphUpload.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         return hip.hipGraphUpload(ctypes.c_void_p(exe), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
@@ -280,6 +285,22 @@ def timed(torch, dist, device, K, one_step, chunk, graph, finish=None):
     return elapsed, kern_ms
 
 
+def episodes(b):
+    """per-env episode counters (every auto-reset increments one)"""
+    import torch
+    from plantos_amd import _capi as CA
+    return b.get_state(parts=("scalars",))["scalars"][:, CA.PE_S_EPISODE].to(torch.int64)
+
+
+def resets_since(torch, dist, b, ep0):
+    """auto-resets performed by all ranks since the counters ep0 were read (outside any
+    timed window: one state read before and one after)"""
+    r = (episodes(b) - ep0).sum().reshape(1).to(torch.int64)
+    if dist:
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+    return int(r.item())
+
+
 def desynchronize(torch, b, seed):
     from plantos_amd import _capi as CA
     st = b.get_state()
@@ -289,27 +310,67 @@ def desynchronize(torch, b, seed):
     b.set_state(scalars=sc)
 
 
-def gather_leg(torch, dist, device, shard, Kg, gather_step, world):
-    """BASELINE config 5's host-boundary leg: Kg steps, each step's packed outputs
-    gathered to rank 0 (RCCL over xGMI; gloo in --selftest), pipelined behind the
-    next step.  Host launches: an RCCL collective inside a captured graph is not
-    exercised on the one-GPU boxes this code is tested on, and a hang there would
-    cost the whole scaling run."""
+class GatherLoop:
+    """One step of BASELINE config 5's host boundary on every rank: the shard steps
+    into one of two output slots and its packed outputs go to rank 0 (RCCL gather,
+    async); rank 0 then turns the PREVIOUS step's gathered slot into the global
+    (obs f32 [W*n, D], reward, terminated, truncated) -- with a codes shard one
+    expansion kernel over the [W, io_bytes] gather buffer -- i.e. what a consumer of
+    the global batch pays, inside the timed window."""
+
+    def __init__(self, shard, actions, rank):
+        self.shard, self.actions, self.root = shard, actions, rank == 0
+        self.prev = None
+
+    def step(self, t):
+        sh = self.shard
+        k = sh.step_gather(self.actions[t % self.actions.shape[0]])
+        if self.prev is not None:
+            self._consume(self.prev)
+        self.prev = k
+
+    def _consume(self, k):
+        sh = self.shard
+        sh.wait(k)  # (the stream waits for the collective; the host does not)
+        if self.root:
+            sh.unpack(sh.gathered(k))
+
+    def finish(self):
+        if self.prev is not None:
+            self._consume(self.prev)
+            self.prev = None
+        self.shard.flush()
+
+
+def gather_leg(torch, dist, device, shard, Kg, loop, world):
+    """BASELINE config 5's host-boundary leg: Kg steps of `loop` (GatherLoop): each
+    step's packed outputs gathered to rank 0 (RCCL over xGMI; gloo in --selftest),
+    pipelined behind the next step, and unpacked there.  Host launches: an RCCL
+    collective inside a captured graph is not exercised on the one-GPU boxes this code
+    is tested on, and a hang there would cost the whole scaling run."""
     for t in range(20):
-        gather_step(t)
-    shard.flush()
+        loop.step(t)
+    loop.finish()
     if device is not None:
         torch.cuda.synchronize()
-    g_el, _ = timed(torch, dist, device, Kg, gather_step, 0, None, shard.flush)
+    g_el, _ = timed(torch, dist, device, Kg, loop.step, 0, None, loop.finish)
     n = shard.n
     per_rank = shard.io_bytes()
     us = g_el / Kg * 1e6
     backend = "RCCL (nccl backend)" if device is not None else "gloo (selftest)"
+    D = shard.batch.obs_dim
     return {"value": n * Kg * world / g_el, "unit": "env-steps/s", "steps": Kg, "us_per_step": us,
+            "payload": ("obs as byte codes (5C+27 B/env) + reward f32 + terminated u8 + truncated u8, expanded "
+                        "on rank 0 by one pe_expand_obs_codes launch into contiguous f32 outputs"
+                        if shard.codes else "obs f32 + reward f32 + terminated u8 + truncated u8; rank 0 "
+                        "concatenates the ranks' parts"),
             "bytes_per_rank_per_step": per_rank, "bytes_gathered_per_step": per_rank * world,
+            "f32_bytes_per_rank_per_step": 4 * n * D + 6 * n,
             "root_ingress_bytes_per_step": per_rank * (world - 1),
             "root_ingress_GBps": per_rank * (world - 1) / (us * 1e-6) / 1e9,
-            "launch": f"{Kg} direct host launches, each step's gather issued async (double-buffered)",
+            "root_expanded_bytes_per_step": (4 * D + 6) * n * world,
+            "launch": f"{Kg} direct host launches, each step's gather issued async (double-buffered), the "
+                      f"previous step's gathered slot unpacked on rank 0",
             "collective": (f"torch.distributed.gather over {backend} to rank 0" + (" (one rank: to itself)" if world == 1
                                                                                      else "")
                            if dist else "none: one rank, nothing to gather (the step into the slot buffers only)")}
@@ -329,6 +390,12 @@ class _SelftestBatch:
 
     def new_io(self):
         return self.torch.zeros(self.io_bytes(), dtype=self.torch.uint8)
+
+    def io_views(self, io):
+        n, D = self.num_envs, self.obs_dim
+        f32 = self.torch.float32
+        return (io[:4 * n * D].view(f32).view(n, D), io[4 * n * D:4 * n * (D + 1)].view(f32),
+                io[4 * n * (D + 1):4 * n * (D + 1) + n], io[4 * n * (D + 1) + n:])
 
     def step(self, actions, io=None):
         n, D = self.num_envs, self.obs_dim
@@ -354,9 +421,8 @@ def selftest_rank(args, world, rank):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     n = 64
     shard = ShardedPlantOS(n, batch_factory=lambda n_, **kw: _SelftestBatch(n_, **kw))
-    acts = torch.zeros(n, dtype=torch.int64)
-    gather = gather_leg(torch, dist if world > 1 else None, None, shard, 10,
-                        lambda k: shard.step_gather(acts), world)
+    acts = torch.zeros((1, n), dtype=torch.int64)
+    gather = gather_leg(torch, dist if world > 1 else None, None, shard, 10, GatherLoop(shard, acts, rank), world)
     ok = True
     if rank == 0:  # every rank's slot arrived, in global env order
         obs = shard.unpack(shard.gathered(0))[0]
@@ -423,8 +489,6 @@ def main():
     def one_step(t):
         b.step(actions[t % T])
 
-    def gather_step(t):
-        shard.step_gather(actions[t % T])  # RCCL gather of (obs, reward, term, trunc), pipelined
 
     def capture(steps):
         if not steps:
@@ -449,8 +513,10 @@ def main():
     for t in range(args.warmup):
         one_step(t)
     torch.cuda.synchronize()
+    ep0 = episodes(b)
     elapsed, kern_ms = timed(torch, dist, device, K, one_step, chunk, graph)
     b.raise_on_errors()
+    resets = resets_since(torch, dist, b, ep0)
     total_steps = n * K * world
     value = total_steps / elapsed
     B = algorithmic_bytes(C, R)
@@ -465,9 +531,11 @@ def main():
         for t in range(200):
             one_step(t)
         torch.cuda.synchronize()
+        dep0 = episodes(b)
         d_el, d_kms = timed(torch, dist, device, Kd, one_step, d_chunk, d_graph)
         d_ach = B * n / (d_kms * 1e-3) / 1e9
         desync = {"value": n * Kd * world / d_el, "unit": "env-steps/s", "steps": Kd,
+                  "resets_in_window": resets_since(torch, dist, b, dep0),
                   "us_per_step": d_el / Kd * 1e6, "kernel_us": d_kms * 1e3, "achieved": d_ach,
                   "frac": d_ach / HBM_PEAK_GBPS, "launch": launch_label(Kd, d_chunk),
                   "note": "every env at its own step count in [0, 1000): ~n/1000 auto-resets per step"}
@@ -476,10 +544,22 @@ def main():
     # BASELINE config 5's host-boundary leg (gather_leg)
     gather = None
     if args.gather_steps > 0:
-        gather = gather_leg(torch, dist, device, shard, args.gather_steps, gather_step, world)
-        gather["episodes"] = "desynchronized (continues the desync window)" if desync is not None else (
-            "as the headline window")
-        b.raise_on_errors()
+        # its own shard (same global ids) whose step keeps the obs as byte codes where the
+        # geometry has a byte-coded sector kernel (config 5's 20x20 / 16 rays does)
+        try:
+            gsh = ShardedPlantOS(n, seed=args.seed, codes=True, batch_factory=lambda n_, **kw: PlantOSBatch(
+                n_, grid_size=G, num_plants=plants, num_obstacles=obstacles, lidar_range=R, lidar_channels=C,
+                device=device, prefetch_every=args.prefetch_every, **kw))
+        except ValueError:
+            gsh = shard
+        if gsh is not shard:
+            desynchronize(torch, gsh.batch, args.seed)
+        gather = gather_leg(torch, dist, device, gsh, args.gather_steps, GatherLoop(gsh, actions, rank), world)
+        gather["episodes"] = "desynchronized"
+        gather["kernel"] = gsh.batch.kernel_name
+        gsh.batch.raise_on_errors()
+        if gsh is not shard:
+            gsh.close()
     if rank == 0:
         sha = lib_sha(_capi.LIB_PATH)
         out = {
@@ -502,6 +582,7 @@ def main():
                        "parallelism": f"env-shard x{world} (independent replicas; RCCL gather leg: 'gather')",
                        "kernel": b.kernel_name,
                        "launch": launch_label(K, chunk)},
+            "resets_in_window": resets,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
                          "bytes_per_env_step": B, "kernel_ms": kern_ms},

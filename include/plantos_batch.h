@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PE_ABI_VERSION 3
+#define PE_ABI_VERSION 4
 
 enum pe_status {
     PE_OK = 0,
@@ -97,7 +97,15 @@ typedef struct pe_config {
                                    one lane per env                                 */
     int32_t prefetch_every;     /* steps between the launches that generate next-episode
                                    maps ahead of time; 0 = no prefetched resets       */
-    int32_t reserved[4];
+    int32_t obs_codes;          /* 1: the step kernel keeps the obs as byte codes (one byte
+                                   per value, every value is one of < 256 table floats):
+                                   pe_step_codes writes them (5C+27 B per env instead of
+                                   4(5C+27)), pe_expand_obs_codes turns them into floats.
+                                   Sector-kernel geometries with a byte-coded tile only
+                                   (C = 16 / R = 6 with G <= 20, C = 64 / R = 6); pe_create
+                                   fails with PE_ERR_ARG elsewhere.  pe_step still writes
+                                   f32 obs on such a handle.  0 (default): off          */
+    int32_t reserved[3];
 } pe_config;
 
 enum pe_map_algo { PE_MAP_ORIGINAL = 0, PE_MAP_MAZE = 1 };
@@ -140,6 +148,28 @@ int pe_step(pe_handle* h, const void* actions, int32_t action_bytes, float* obs,
             uint8_t* terminated, uint8_t* truncated, float* terminal_obs_or_null,
             double* episode_return_or_null, int32_t* episode_length_or_null,
             int32_t* terminal_info_or_null, void* stream);
+
+/* pe_step with the obs as byte codes (handles created with obs_codes = 1):
+ * obs_codes u8[n, D] instead of f32[n, D]; every other argument as pe_step.  This is
+ * the host-boundary form of a sharded job (plantos_amd/shard.py): ranks gather 5C+27 B
+ * per env instead of 4(5C+27), and the root expands the codes once. */
+int pe_step_codes(pe_handle* h, const void* actions, int32_t action_bytes, uint8_t* obs_codes, float* reward,
+                  uint8_t* terminated, uint8_t* truncated, float* terminal_obs_or_null,
+                  double* episode_return_or_null, int32_t* episode_length_or_null,
+                  int32_t* terminal_info_or_null, void* stream);
+
+/* The float of every obs byte code (table f32[256], host memory; unused codes 0.0). */
+int pe_obs_code_table(const pe_handle* h, float* table);
+
+/* Expand `blocks` packed code buffers into contiguous outputs.  Block b starts at
+ * src + b * src_stride (bytes, a multiple of 16) and holds codes u8[rows, D], then at
+ * the next multiple of 16 bytes reward f32[rows], terminated u8[rows], truncated
+ * u8[rows] (the io layout of plantos_amd's code-mode batches); outputs: obs
+ * f32[blocks * rows, D] and (each may be NULL) reward f32 / terminated u8 / truncated
+ * u8 [blocks * rows], in block order.  Any handle of the same geometry gives the same
+ * table (e.g. the root rank's shard expanding every rank's gathered codes). */
+int pe_expand_obs_codes(const pe_handle* h, int32_t blocks, int32_t rows, const uint8_t* src, int64_t src_stride,
+                        float* obs, float* reward, uint8_t* terminated, uint8_t* truncated, void* stream);
 
 /* info columns (pe_info) for all envs: int32[n, PE_NINFO]. */
 int pe_get_info(pe_handle* h, int32_t* info, void* stream);

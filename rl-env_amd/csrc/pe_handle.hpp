@@ -16,6 +16,7 @@ struct pe_handle {
   int variant;
   int tile_codes;    // the sector kernel's obs tile holds byte codes (pe_step_quad<..., BT>); so do the
                      // prefetched records' obs rows
+  int obs_codes;     // pe_config.obs_codes: pe_step_codes allowed (implies tile_codes)
   const char* kname;
   char kname_buf[64];  // kname with the envs-per-workgroup suffix (small batches)
   void* cur_mem;     // CurriculumWrapper records (pe_curriculum_enable), or NULL
@@ -23,6 +24,9 @@ struct pe_handle {
   int quad_waves;    // waves per workgroup of the sector kernel (4; 8 via PE_QUAD_WAVES in debug builds)
   int quad_epb;      // envs per workgroup of the sector kernel (64; 16 / 32 for small batches, C16R6 one-word)
   int stagger;       // sector-kernel start delay per block quarter (PE_STAGGER, debug builds only)
+  int pipe_wpc;      // > 0: the persistent pipelined sector kernel (pe_step_pipe), this many
+                     // workgroups per CU; 0: pe_step_quad
+  int num_cus;       // the device's CUs (the persistent grid)
   int coop_max_done; // wave-cooperative auto-resets up to this many done envs per block (pe_coop.hpp;
                      // pe_config.coop_max_done)
   pe::Prefetch pf;   // prefetched resets (pf.scal == NULL: off)

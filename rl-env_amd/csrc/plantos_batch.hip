@@ -42,6 +42,7 @@ struct StepArgs {
   int coop_max_done;  // step kernel: wave-cooperative resets up to this many done envs per block
   const void* actions;
   float* obs;
+  uint8_t* obs_codes;   // byte-coded tile kernels: the obs as codes (pe_step_codes) instead of obs
   float* reward;
   uint8_t* term;
   uint8_t* trunc;
@@ -123,6 +124,38 @@ __device__ inline void build_obs_fresh(const StepArgs& a, const uint64_t* sg, co
       const bool in = gx >= 0 && gx < g.G && gy >= 0 && gy < g.G;       // :307-311
       const bool rover = lx == 2 && ly == 2 && !(s.flags & F_NOROOM);
       out[5 * C + 2 + 5 * lx + ly] = !in ? tvis[10] : (rover ? tvis[1] : tvis[0]);
+    }
+}
+
+// The same obs as byte codes (pe_coop.hpp ObsW<uint8_t>: dist r -> r, one-hot 0 / 1 ->
+// 0 / R+1, vis v -> kCodeVis + v, pos x -> kCodePos + x).
+__device__ inline void build_obs_fresh_codes(const StepArgs& a, const uint64_t* sg, const Scal& s, uint8_t* out,
+                                             const signed char* ldx, const signed char* ldy) {
+  const Geo& g = a.g;
+  const int R = g.R, C = g.C, x = s.x, y = s.y;
+  for (int i = 0; i < C; ++i) {
+    int dist = R, ent = EMPTY;
+    for (int r = 1; r <= R; ++r) {
+      const int cx = x + ldx[i * R + r - 1];
+      const int cy = y + ldy[i * R + r - 1];
+      const int code = (cx >= 0 && cx < g.G) ? img_code(sg, g, cx, cy + R) : OBST;  // :271-284
+      if (code != EMPTY) {
+        dist = r;
+        ent = code;
+        break;
+      }
+    }
+    out[5 * i] = (uint8_t)dist;
+    for (int k = 0; k < 4; ++k) out[5 * i + 1 + k] = (uint8_t)(ent == k ? R + 1 : 0);
+  }
+  out[5 * C] = (uint8_t)(kCodePos + x);
+  out[5 * C + 1] = (uint8_t)(kCodePos + y);
+  for (int lx = 0; lx < 5; ++lx)
+    for (int ly = 0; ly < 5; ++ly) {
+      const int gx = x + lx - 2, gy = y + ly - 2;
+      const bool in = gx >= 0 && gx < g.G && gy >= 0 && gy < g.G;       // :307-311
+      const bool rover = lx == 2 && ly == 2 && !(s.flags & F_NOROOM);
+      out[5 * C + 2 + 5 * lx + ly] = (uint8_t)(kCodeVis + (!in ? 10 : (rover ? 1 : 0)));
     }
 }
 
@@ -323,6 +356,26 @@ __device__ __forceinline__ void store_tile_codes(const uint8_t* codes, const flo
   } else {
     for (int k = t0; k < total; k += nt) dst[k] = ctab[codes[k]];
   }
+}
+
+// The byte-coded tile as it is (pe_step_codes): [valid x D] codes, 16-B sc1 stores
+// where the destination allows, bytes for the rest.
+__device__ __forceinline__ void store_tile_bytes(const uint8_t* codes, uint8_t* dst, int valid, int D, int t0,
+                                                 int nt) {
+  const int total = valid * D;
+  int head = 0;
+  if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+    const int n16 = total >> 4;
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u* sv = reinterpret_cast<const v4u*>(codes);
+    v4u* d4 = reinterpret_cast<v4u*>(dst);
+    for (int k = t0; k < n16; k += nt) {
+      const v4u v = sv[k];
+      asm volatile("global_store_dwordx4 %0, %1, off " PE_OBS_STORE_ASM "\n\ts_nop 1" ::"v"(d4 + k), "v"(v) : "memory");
+    }
+    head = n16 << 4;
+  }
+  for (int k = head + t0; k < total; k += nt) dst[k] = codes[k];
 }
 
 // ------------------------------------------------------------------ kernels
@@ -889,8 +942,235 @@ __device__ __forceinline__ void quad_done_obs(const void* ka, int tile_off, int 
   const uint64_t* sg = BT ? a.st.grid + e * g.gstride : reinterpret_cast<const uint64_t*>(row + ((lane * g.D) & 1));
   const signed char* lldx = reinterpret_cast<const signed char*>(smem + kTabFloats);
   PE_RSTAMP(4);
-  if (done) build_obs_fresh(a, sg, unpack(sp), a.obs + e * g.D, smem, smem + 72, smem + 328, lldx, lldx + g.C * g.R);
+  if (done) {
+    if (BT && a.obs_codes)
+      build_obs_fresh_codes(a, sg, unpack(sp), a.obs_codes + e * g.D, lldx, lldx + g.C * g.R);
+    else
+      build_obs_fresh(a, sg, unpack(sp), a.obs + e * g.D, smem, smem + 72, smem + 328, lldx, lldx + g.C * g.R);
+  }
   PE_RSTAMP(5);
+}
+
+// The action's move / watering decode (plantos_env.py:166, 186-195) and the window
+// coordinates it implies, from the scalars before the step.
+struct QuadMove {
+  bool mv, water, bad, inb;      // move / water / reference IndexError / target in bounds
+  int dxm, dym, nx, ny, nyc;     // direction, target, target column clamped to the map
+  int yb, ybv, cell_o, cell_n;   // window's first padded grid / visit column, old / new cell
+};
+template <bool ONEWORD>
+__device__ __forceinline__ QuadMove quad_move(const Scal& s, int64_t action, int G) {
+  QuadMove m;
+  m.mv = false;
+  m.water = false;
+  m.bad = false;
+  m.dxm = 0;
+  m.dym = 0;
+  if (action < 4) {                                              // plantos_env.py:166
+    const int64_t ai = action < 0 ? action + 4 : action;         // Python negative index
+    if (ai < 0) {
+      m.bad = true;                                              // reference IndexError
+    } else {
+      m.mv = true;                                               // :186 N,E,S,W
+      m.dxm = ai == 0 ? -1 : (ai == 2 ? 1 : 0);
+      m.dym = ai == 1 ? 1 : (ai == 3 ? -1 : 0);
+    }
+  } else {
+    m.water = true;
+  }
+  m.nx = s.x + m.dxm;
+  m.ny = s.y + m.dym;
+  m.inb = m.mv && m.nx >= 0 && m.nx < G && m.ny >= 0 && m.ny < G;  // :193-195
+  return m;
+}
+// (the window coordinates: separate, so that the kernels compute them where they did)
+template <bool ONEWORD>
+__device__ __forceinline__ void quad_move_cells(QuadMove& m, const Scal& s, int G) {
+  m.nyc = m.inb ? m.ny : s.y;
+  m.yb = ONEWORD ? 0 : (s.y > 0 ? s.y - 1 : 0);
+  m.ybv = s.y > 0 ? s.y - 1 : 0;
+  m.cell_o = s.x * G + s.y;
+  m.cell_n = m.nx * G + m.nyc;
+}
+
+// The compute phase of the sector kernels (pe_step_quad, pe_step_pipe), between the
+// window barrier and the done barrier: every wave re-derives the transition
+// (plantos_env.py:160-222) from the LDS window, marches its sector of rays and writes
+// its part of the env's obs row into the LDS tile; the commit wave (NW-1) stores the
+// state.  done / wfix: the env ended this step / its last watering is not stored.
+// eo / en / cthr: the explored-bitmap words (F_EXPL_BITMAP) and the CurriculumWrapper
+// threshold, loaded by the caller with round 2, or (LX) here by the commit wave in the
+// modes that need them -- the persistent kernel keeps other loads in flight here, and
+// a wait for a value loaded one iteration earlier is a vmcnt(0).
+template <int C, int R, bool ONEWORD, int NW, bool BT, bool RT, bool LX = false>
+__device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* lrow, const uint32_t* lvis,
+                                             typename std::conditional<BT, uint8_t, float>::type* rows,
+                                             const float* tdist, const float* tpos, const float* tvis, int lane,
+                                             int wv, int64_t e, bool live, int Cr, int Rr, const QuadMove& m,
+                                             uint32_t eo, uint32_t en, double cthr, Scal& s, double& ret,
+                                             bool& done, bool& wfix) {
+  using OT = typename std::conditional<BT, uint8_t, float>::type;
+  constexpr int LS = kQuadEnvs, CW = NW - 1;
+  const Geo& g = a.g;
+  // the rules by value: a per-lane choice between two fields of a referenced struct
+  // became a per-lane address select and a VMEM load of the chosen double
+  const Rules rl = a.rl;
+  const State& st = a.st;
+  const uint64_t* gb = st.grid + e * g.gstride;
+  done = false;
+  wfix = false;
+  s.step = s.step < 65535 ? s.step + 1 : 65535;                  // :162
+  bool ok = false, watered = false, wet_hyd = false;
+  uint32_t n = 0u;
+  int dxv = 0;
+  double h = 0.0;
+  if (m.mv) {
+    const uint64_t rt = lrow[(Rr + 1 + m.dxm) * LS + lane];
+    ok = m.inb && ((rt >> (2 * (m.nyc + Rr - m.yb))) & 3u) != OBST;     // :193-195 (plants walkable)
+    if (ok) {
+      n = (lvis[(3 + m.dxm) * LS + lane] >> (4 * (m.nyc + 2 - m.ybv))) & 15u;
+      h = n == 0u ? rl.r_exploration : rl.r_revisit;              // :197, 204-207
+      dxv = m.dxm;
+    } else {
+      s.flags |= F_COLLIDED;                                      // :209
+      s.coll = s.coll < 65535 ? s.coll + 1 : 65535;               // :210
+      h = rl.r_invalid;                                           // :211
+    }
+  } else if (m.water) {
+    const uint64_t rc = lrow[(Rr + 1) * LS + lane];
+    const int cd = (int)((rc >> (2 * (s.y + Rr - m.yb))) & 3u);
+    if (cd == THIRSTY) {                                          // fork plantos_env_new.py:237-240
+      watered = true;
+      h = rl.r_goal;
+    } else if (cd == HYD) {                                       // fork :241-242 (root raises)
+      wet_hyd = true;
+      h = rl.r_mistake;
+    } else {
+      h = rl.r_water_empty;                                       // :221-222
+    }
+  }
+  const int xp = s.x + dxv, yp = ok ? m.ny : s.y;
+  const uint32_t nib = n < 15u ? n + 1u : 15u;                    // :203
+  OT* row = rows + lane * g.D;
+  if (live) {
+    const int kc = dxv + Rr + 1;
+    const int sh = 2 * (yp - m.yb);
+    const int vs = 4 * (yp - m.ybv);
+    if constexpr (RT) {
+      quad_rays_rt<OT>(lrow, st.ldxy, wv * Cr / NW, (wv + 1) * Cr / NW, Rr, lane, kc, sh, watered, row, tdist);
+    } else {
+      sector_rays<C, R, NW>(wv, lrow, lane, kc, sh, watered, row, tdist);
+    }
+    // slice rows and position go to the non-commit waves (the commit wave is the laggard)
+    if (wv != CW)
+      for (int lx = wv; lx < 5; lx += NW - 1) quad_slice_row(lvis, lane, lx, dxv, vs, ok, nib, Cr, row, tvis);
+    if (wv == (NW == 4 ? 2 : 5)) {                                // :294-296
+      if constexpr (BT) {
+        row[5 * Cr] = (uint8_t)(kCodePos + xp);
+        row[5 * Cr + 1] = (uint8_t)(kCodePos + yp);
+      } else {
+        row[5 * Cr] = tpos[xp];
+        row[5 * Cr + 1] = tpos[yp];
+      }
+    }
+    if (wv == CW) {
+      // ---- commit (plantos_env.py:160-222)
+      uint32_t wo = eo, wn = en;  // explored-bitmap words after the move (bitmap mode)
+      if (ok) {
+        if (s.flags & F_EXPL_BITMAP) {                            // explored[old]=1, [new]=2 (:198-200)
+          if constexpr (LX) {  // (loaded where used: a copy outside the branch would wait for it)
+            eo = st.expl[e * g.estride + (m.cell_o >> 5)];
+            en = st.expl[e * g.estride + (m.cell_n >> 5)];
+            wo = eo;
+            wn = en;
+          }
+          const uint32_t bo = 1u << (m.cell_o & 31), bn = 1u << (m.cell_n & 31);
+          if ((m.cell_o >> 5) == (m.cell_n >> 5)) {
+            if (!(wo & bo)) { wo |= bo; s.expl++; }
+            if (!(wo & bn)) { wo |= bn; s.expl++; }
+          } else {
+            if (!(wo & bo)) { wo |= bo; s.expl++; }
+            if (!(wn & bn)) { wn |= bn; s.expl++; }
+          }
+        } else if (n == 0u) {
+          s.expl++;  // derived mode: explored[new] was 0 iff never visited
+        }
+      }
+      if (m.bad) {
+        s.flags |= F_POISON_ACT;
+        atomicOr(st.err_bits, F_POISON_ACT);
+      }
+      if (wet_hyd && !(s.flags & F_POISON_HYD)) {
+        s.flags |= F_POISON_HYD;
+        atomicOr(st.err_bits, F_POISON_HYD);
+      }
+      const int ox = s.x;
+      s.x = xp;                                                   // :199
+      s.y = yp;
+      double rew = rl.r_step;                                     // :164
+      rew += h;
+      bool term = s.expl >= s.total;                              // :176, 244-246, 331
+      const bool trunc = s.step >= rl.max_steps;                  // :177
+      if (term && !(s.flags & F_BONUS)) {                         // :179-181
+        rew += rl.r_complete;
+        s.flags |= F_BONUS;
+      }
+      if (st.cur) {
+        if constexpr (LX) cthr = st.cur[e].thr;  // CurriculumWrapper threshold
+        term = curriculum_hit(st.cur, e, cthr, s.expl, s.total, rl.cur_term) || term;  // A2C_training.py:101-103
+      }
+      done = term || trunc;  // terminal outputs; the reset itself only with autoreset
+      // an env about to be auto-reset gets new grid and visit rows: its last move /
+      // watering is not stored (the terminal info accounts for the watering), so no
+      // store of this step can land after the reset's (unless the curriculum
+      // carries the visits over)
+      wfix = watered && done && a.autoreset && !st.cur;
+      if (!(done && a.autoreset && !st.cur)) {
+        if (ok) {
+          // the byte holding the target's visit nibble (padded column p), rebuilt from
+          // the window of row nx in LDS (padded nibbles ybv..ybv+7 hold both of its
+          // nibbles): one byte store, no read of the word from memory
+          const int p = m.ny + 2, b = p >> 1;
+          const uint32_t wnew = (lvis[(3 + m.dxm) * LS + lane] & ~(0xFu << (4 * (p - m.ybv)))) | (nib << (4 * (p - m.ybv)));
+          st_wt(reinterpret_cast<uint8_t*>(st.vis + e * g.vstride + (int64_t)m.nx * g.NW) + b,
+                (uint8_t)(wnew >> (4 * (2 * b - m.ybv))));
+          visit_bump_exact(st, g, e, m.cell_n, n);
+          if (s.flags & F_EXPL_BITMAP) {
+            uint32_t* ep_o = st.expl + e * g.estride + (m.cell_o >> 5);
+            uint32_t* ep_n = st.expl + e * g.estride + (m.cell_n >> 5);
+            if (wo != eo) *ep_o = wo;
+            if ((m.cell_o >> 5) != (m.cell_n >> 5) && wn != en) *ep_n = wn;
+          }
+        }
+        if (watered) {
+          const int bit = 2 * (s.y + Rr);
+          if constexpr (ONEWORD) {
+            st_wt(const_cast<uint64_t*>(gb) + ox, (uint64_t)(lrow[(Rr + 1) * LS + lane] & ~(1ull << bit)));  // code 3 -> 2
+          } else {
+            // the byte holding the cell's code (padded column c; its 4 cells lie in the
+            // window of row x, padded columns yb..yb+31, for R >= 2)
+            const int c = s.y + Rr, B = c >> 2;
+            const uint64_t wr = lrow[(Rr + 1) * LS + lane] & ~(1ull << (2 * (c - m.yb)));  // code 3 -> 2
+            st_wt(reinterpret_cast<uint8_t*>(const_cast<uint64_t*>(gb) + (int64_t)ox * g.WPR) + B,
+                  (uint8_t)(wr >> (2 * (4 * B - m.yb))));
+          }
+        }
+      }
+      ret += rew;
+      st_wt(a.reward + e, (float)rew);
+      st_wt(a.term + e, (uint8_t)term);
+      st_wt(a.trunc + e, (uint8_t)trunc);
+      if (done) {  // Monitor's episode return / length of the ended episode
+        if (a.ep_ret_out) st_wt(a.ep_ret_out + e, ret);
+        if (a.ep_len_out) st_wt(a.ep_len_out + e, (int32_t)s.step);
+      }
+      // an env about to be auto-reset: its reset path stores the new episode's scalars
+      if (!(done && a.autoreset && !st.cur)) {
+        st_wt(st.ep_ret + e, ret);
+        st_wt(st.scal + e, pack(s));
+      }
+    }
+  }
 }
 
 // BT: byte-coded obs tile (pe_coop.hpp ObsW<uint8_t>): [64 x D] bytes instead of
@@ -899,10 +1179,7 @@ __device__ __forceinline__ void quad_done_obs(const void* ka, int tile_off, int 
 // EPB: envs per workgroup (64; 16 / 32 for small batches: more workgroups, so that
 // a batch of a few thousand envs spreads over every CU -- lanes >= EPB idle).  The
 // LDS layout keeps the 64-env stride LS whatever EPB.
-// W2: unused (every instantiation false) -- a compile-time variant for rows of exactly 2
-// words measured slower (profiles/r3ak/rows_of_two_words_W2.diff);
-// kept only so that this library is byte-identical to the one measured in profiles/r3am_*.
-template <int C, int R, bool ONEWORD, int NW, bool BT = false, int EPB = kQuadEnvs, bool W2 = false>
+template <int C, int R, bool ONEWORD, int NW, bool BT = false, int EPB = kQuadEnvs>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs (small-batch EPB: one workgroup per CU, no cap); NW=4: <= 128 VGPRs (4 workgroups per CU: G=25 13.1 -> 10.5 us; 1-word C16: 122 -> 104 VGPRs)
   // C == 0 (R == 0): the runtime-(C, R) sector kernel (quad_rays_rt): C, R from the
   // geometry (up to kRtCMax / kRtRMax), the LDS layout sized at run time
@@ -986,29 +1263,13 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   if constexpr (BT) {
     if (threadIdx.x < 256) ctab[threadIdx.x] = obs_code_value(st.tab, R, g.G, (int)threadIdx.x);
   }
-  const Tables* ltab = reinterpret_cast<const Tables*>(smem);
   Scal s = unpack(sw);
 #ifdef PE_STAMPS
   if ((int)(s.x + lw.x) == -12345) g_stamps[0] = 1;  // consume round 1 before the stamp
 #endif
   PE_STAMP(1);
   const int64_t action = ash ? (int64_t)(((uint64_t)(uint32_t)ahi << 32) | (uint32_t)alo) : (int64_t)alo;
-  bool mv = false, water = false, bad = false;
-  int dxm = 0, dym = 0;
-  if (action < 4) {                                              // plantos_env.py:166
-    const int64_t ai = action < 0 ? action + 4 : action;         // Python negative index
-    if (ai < 0) {
-      bad = true;                                                // reference IndexError
-    } else {
-      mv = true;                                                 // :186 N,E,S,W
-      dxm = ai == 0 ? -1 : (ai == 2 ? 1 : 0);
-      dym = ai == 1 ? 1 : (ai == 3 ? -1 : 0);
-    }
-  } else {
-    water = true;
-  }
-  const int nx = s.x + dxm, ny = s.y + dym;
-  const bool inb = mv && nx >= 0 && nx < g.G && ny >= 0 && ny < g.G;  // :193-195
+  QuadMove m = quad_move<ONEWORD>(s, action, g.G);
   // A block whose only env to truncate this step is known from its step count
   // (:177, the steady state of desynchronized episodes: ~6 % of the blocks each
   // step): that env's prefetched record -- and, small grids, its current rows for the
@@ -1035,11 +1296,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
     if (BT && wv == CW && npred == 1)
       pf_stage_issue(a.pf, st, g, e0 + (__ffsll((unsigned long long)pm) - 1), stage, lane, stage_info);
   };
-  const int nyc = inb ? ny : s.y;
-  const int yb = ONEWORD ? 0 : (s.y > 0 ? s.y - 1 : 0);
-  const int ybv = s.y > 0 ? s.y - 1 : 0;
-  const uint64_t* gb = st.grid + e * g.gstride;
-  const int cell_o = s.x * g.G + s.y, cell_n = nx * g.G + nyc;
+  quad_move_cells<ONEWORD>(m, s, g.G);
 
   // Early record (f32-tile one-word kernels): a block whose ONLY env to truncate this
   // step is known from its step count (:177; ~6 % of the blocks of a desynchronized
@@ -1233,9 +1490,9 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   double cthr = 0.0;
   if (live && wv == CW) {
     if (st.cur) cthr = st.cur[e].thr;  // CurriculumWrapper threshold
-    if (inb && (s.flags & F_EXPL_BITMAP)) {
-      eo = st.expl[e * g.estride + (cell_o >> 5)];
-      en = st.expl[e * g.estride + (cell_n >> 5)];
+    if (m.inb && (s.flags & F_EXPL_BITMAP)) {
+      eo = st.expl[e * g.estride + (m.cell_o >> 5)];
+      en = st.expl[e * g.estride + (m.cell_n >> 5)];
     }
   }
 #ifdef PE_STAMPS
@@ -1261,150 +1518,9 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // phase, instead of in the done path: the commit wave then waited for them before
   // re-using their data registers -- desynchronized 11.12 -> 12.05 us, synchronized
   // 9.47 -> 9.59; profiles/r3i_ab_*.jsonl.)
-  s.step = s.step < 65535 ? s.step + 1 : 65535;                  // :162
-  bool ok = false, watered = false, wet_hyd = false;
-  uint32_t n = 0u;
-  int dxv = 0;
-  double h = 0.0;
-  if (mv) {
-    const uint64_t rt = lrow[(Rr + 1 + dxm) * LS + lane];
-    ok = inb && ((rt >> (2 * (nyc + Rr - yb))) & 3u) != OBST;     // :193-195 (plants walkable)
-    if (ok) {
-      n = (lvis[(3 + dxm) * LS + lane] >> (4 * (nyc + 2 - ybv))) & 15u;
-      h = n == 0u ? rl.r_exploration : rl.r_revisit;              // :197, 204-207
-      dxv = dxm;
-    } else {
-      s.flags |= F_COLLIDED;                                      // :209
-      s.coll = s.coll < 65535 ? s.coll + 1 : 65535;               // :210
-      h = rl.r_invalid;                                           // :211
-    }
-  } else if (water) {
-    const uint64_t rc = lrow[(Rr + 1) * LS + lane];
-    const int cd = (int)((rc >> (2 * (s.y + Rr - yb))) & 3u);
-    if (cd == THIRSTY) {                                          // fork plantos_env_new.py:237-240
-      watered = true;
-      h = rl.r_goal;
-    } else if (cd == HYD) {                                       // fork :241-242 (root raises)
-      wet_hyd = true;
-      h = rl.r_mistake;
-    } else {
-      h = rl.r_water_empty;                                       // :221-222
-    }
-  }
-  const int xp = s.x + dxv, yp = ok ? ny : s.y;
-  const uint32_t nib = n < 15u ? n + 1u : 15u;                    // :203
-  OT* row = rows + lane * g.D;
   bool done = false, wfix = false;
-  if (live) {
-    const int kc = dxv + Rr + 1;
-    const int sh = 2 * (yp - yb);
-    const int vs = 4 * (yp - ybv);
-    if constexpr (RT) {
-      quad_rays_rt<OT>(lrow, st.ldxy, wv * Cr / NW, (wv + 1) * Cr / NW, Rr, lane, kc, sh, watered, row, tdist);
-    } else {
-      sector_rays<C, R, NW>(wv, lrow, lane, kc, sh, watered, row, tdist);
-    }
-    // slice rows and position go to the non-commit waves (the commit wave is the laggard)
-    if (wv != CW)
-      for (int lx = wv; lx < 5; lx += NW - 1) quad_slice_row(lvis, lane, lx, dxv, vs, ok, nib, Cr, row, tvis);
-    if (wv == (NW == 4 ? 2 : 5)) {                                // :294-296
-      if constexpr (BT) {
-        row[5 * Cr] = (uint8_t)(kCodePos + xp);
-        row[5 * Cr + 1] = (uint8_t)(kCodePos + yp);
-      } else {
-        row[5 * Cr] = tpos[xp];
-        row[5 * Cr + 1] = tpos[yp];
-      }
-    }
-    if (wv == CW) {
-      // ---- commit (plantos_env.py:160-222)
-      uint32_t wo = eo, wn = en;  // explored-bitmap words after the move (bitmap mode)
-      if (ok) {
-        if (s.flags & F_EXPL_BITMAP) {                            // explored[old]=1, [new]=2 (:198-200)
-          const uint32_t bo = 1u << (cell_o & 31), bn = 1u << (cell_n & 31);
-          if ((cell_o >> 5) == (cell_n >> 5)) {
-            if (!(wo & bo)) { wo |= bo; s.expl++; }
-            if (!(wo & bn)) { wo |= bn; s.expl++; }
-          } else {
-            if (!(wo & bo)) { wo |= bo; s.expl++; }
-            if (!(wn & bn)) { wn |= bn; s.expl++; }
-          }
-        } else if (n == 0u) {
-          s.expl++;  // derived mode: explored[new] was 0 iff never visited
-        }
-      }
-      if (bad) {
-        s.flags |= F_POISON_ACT;
-        atomicOr(st.err_bits, F_POISON_ACT);
-      }
-      if (wet_hyd && !(s.flags & F_POISON_HYD)) {
-        s.flags |= F_POISON_HYD;
-        atomicOr(st.err_bits, F_POISON_HYD);
-      }
-      const int ox = s.x;
-      s.x = xp;                                                   // :199
-      s.y = yp;
-      double rew = rl.r_step;                                     // :164
-      rew += h;
-      bool term = s.expl >= s.total;                              // :176, 244-246, 331
-      const bool trunc = s.step >= rl.max_steps;                  // :177
-      if (term && !(s.flags & F_BONUS)) {                         // :179-181
-        rew += rl.r_complete;
-        s.flags |= F_BONUS;
-      }
-      if (st.cur) term = curriculum_hit(st.cur, e, cthr, s.expl, s.total, rl.cur_term) || term;  // A2C_training.py:101-103
-      done = term || trunc;  // terminal outputs; the reset itself only with autoreset
-      // an env about to be auto-reset gets new grid and visit rows: its last move /
-      // watering is not stored (the terminal info accounts for the watering), so no
-      // store of this step can land after the reset's (unless the curriculum
-      // carries the visits over)
-      wfix = watered && done && a.autoreset && !st.cur;
-      if (!(done && a.autoreset && !st.cur)) {
-        if (ok) {
-          // the byte holding the target's visit nibble (padded column p), rebuilt from
-          // the window of row nx in LDS (padded nibbles ybv..ybv+7 hold both of its
-          // nibbles): one byte store, no read of the word from memory
-          const int p = ny + 2, b = p >> 1;
-          const uint32_t wnew = (lvis[(3 + dxm) * LS + lane] & ~(0xFu << (4 * (p - ybv)))) | (nib << (4 * (p - ybv)));
-          st_wt(reinterpret_cast<uint8_t*>(st.vis + e * g.vstride + (int64_t)nx * g.NW) + b,
-                (uint8_t)(wnew >> (4 * (2 * b - ybv))));
-          visit_bump_exact(st, g, e, cell_n, n);
-          if (s.flags & F_EXPL_BITMAP) {
-            uint32_t* ep_o = st.expl + e * g.estride + (cell_o >> 5);
-            uint32_t* ep_n = st.expl + e * g.estride + (cell_n >> 5);
-            if (wo != eo) *ep_o = wo;
-            if ((cell_o >> 5) != (cell_n >> 5) && wn != en) *ep_n = wn;
-          }
-        }
-        if (watered) {
-          const int bit = 2 * (s.y + Rr);
-          if constexpr (ONEWORD) {
-            st_wt(const_cast<uint64_t*>(gb) + ox, (uint64_t)(lrow[(Rr + 1) * LS + lane] & ~(1ull << bit)));  // code 3 -> 2
-          } else {
-            // the byte holding the cell's code (padded column c; its 4 cells lie in the
-            // window of row x, padded columns yb..yb+31, for R >= 2)
-            const int c = s.y + Rr, B = c >> 2;
-            const uint64_t wr = lrow[(Rr + 1) * LS + lane] & ~(1ull << (2 * (c - yb)));  // code 3 -> 2
-            st_wt(reinterpret_cast<uint8_t*>(const_cast<uint64_t*>(gb) + (int64_t)ox * g.WPR) + B,
-                  (uint8_t)(wr >> (2 * (4 * B - yb))));
-          }
-        }
-      }
-      ret += rew;
-      st_wt(a.reward + e, (float)rew);
-      st_wt(a.term + e, (uint8_t)term);
-      st_wt(a.trunc + e, (uint8_t)trunc);
-      if (done) {  // Monitor's episode return / length of the ended episode
-        if (a.ep_ret_out) st_wt(a.ep_ret_out + e, ret);
-        if (a.ep_len_out) st_wt(a.ep_len_out + e, (int32_t)s.step);
-      }
-      // an env about to be auto-reset: its reset path stores the new episode's scalars
-      if (!(done && a.autoreset && !st.cur)) {
-        st_wt(st.ep_ret + e, ret);
-        st_wt(st.scal + e, pack(s));
-      }
-    }
-  }
+  quad_compute<C, R, ONEWORD, NW, BT, RT>(a, lrow, lvis, rows, tdist, tpos, tvis, lane, wv, e, live, Cr, Rr, m, eo, en,
+                                          cthr, s, ret, done, wfix);
   PE_STAMP(4);
   // ---- DummyVecEnv auto-reset (rare): commit wave, after the whole obs row is in LDS
   // any env of the block done (the usual answer: no)?  The commit wave's done mask
@@ -1448,15 +1564,21 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // before re-using a store's data registers)
   if constexpr (CM >= 64) {  // long rows: the commit wave's share pays for its wait (64x64: 33.2 -> 32.7 us)
     if (wv == CW) __builtin_amdgcn_s_waitcnt(0x0F70);  // tracked vmcnt(0): no wait inside the loop
-    if constexpr (BT)
-      store_tile_codes(rows, ctab, a.obs + e0 * g.D, (int)valid, g.D, (int)threadIdx.x, (int)blockDim.x);
-    else
+    if constexpr (BT) {
+      if (a.obs_codes)
+        store_tile_bytes(rows, a.obs_codes + e0 * g.D, (int)valid, g.D, (int)threadIdx.x, (int)blockDim.x);
+      else
+        store_tile_codes(rows, ctab, a.obs + e0 * g.D, (int)valid, g.D, (int)threadIdx.x, (int)blockDim.x);
+    } else
       store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D);
   } else {
     if (wv != CW) {
-      if constexpr (BT)
-        store_tile_codes(rows, ctab, a.obs + e0 * g.D, (int)valid, g.D, (int)threadIdx.x, 64 * (NW - 1));
-      else
+      if constexpr (BT) {
+        if (a.obs_codes)
+          store_tile_bytes(rows, a.obs_codes + e0 * g.D, (int)valid, g.D, (int)threadIdx.x, 64 * (NW - 1));
+        else
+          store_tile_codes(rows, ctab, a.obs + e0 * g.D, (int)valid, g.D, (int)threadIdx.x, 64 * (NW - 1));
+      } else
         store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D, (int)threadIdx.x, 64 * (NW - 1));
     }
   }
@@ -1474,6 +1596,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
 #endif
   PE_STAMP(7);
 }
+
+#include "pe_pipe.hpp"
 
 // ---------------------------------------------------------------- pe_step_wave
 // The fused step for every geometry without a compile-time sector kernel (any
@@ -2286,6 +2410,44 @@ __global__ void pe_synth_kernel(int n, uint64_t seed, uint32_t env_off, uint32_t
 
 }  // namespace
 
+// pe_expand_obs_codes: blocks x rows packed code buffers (codes u8 [rows, D] | reward
+// f32 | terminated | truncated, block b at src + b * stride) -> contiguous f32 obs
+// (+ the other outputs).  Grid: (x: 16-B output chunks, y: block); one u32 of 4 codes
+// per thread through the LDS code table, one 16-B store.
+__global__ __launch_bounds__(256) void pe_expand_codes_kernel(const Tables* tab, int R, int G, int D, int rows,
+                                                              const uint8_t* src, int64_t stride, float* obs,
+                                                              float* rew, uint8_t* te, uint8_t* tr) {
+  __shared__ float ctab[256];
+  ctab[threadIdx.x] = obs_code_value(tab, R, G, (int)threadIdx.x);
+  __syncthreads();
+  const int b = blockIdx.y;
+  const uint8_t* sb = src + (int64_t)b * stride;
+  const int64_t nc = (int64_t)rows * D;  // codes per block
+  float* ob = obs + (int64_t)b * nc;
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 4-code group
+  if ((nc & 3) == 0) {
+    if (4 * k < nc) {
+      const uint32_t c = *reinterpret_cast<const uint32_t*>(sb + 4 * k);
+      float4 v;
+      v.x = ctab[c & 255u];
+      v.y = ctab[(c >> 8) & 255u];
+      v.z = ctab[(c >> 16) & 255u];
+      v.w = ctab[c >> 24];
+      *reinterpret_cast<float4*>(ob + 4 * k) = v;
+    }
+  } else {
+    for (int64_t j = 4 * k; j < 4 * k + 4 && j < nc; ++j) ob[j] = ctab[sb[j]];
+  }
+  // the per-env outputs: one env per thread of the first ceil(rows / 256) workgroups
+  if (k < rows) {
+    const int64_t ro = (nc + 15) & ~(int64_t)15;
+    const int64_t o = (int64_t)b * rows + k;
+    if (rew) rew[o] = reinterpret_cast<const float*>(sb + ro)[k];
+    if (te) te[o] = sb[ro + 4 * (int64_t)rows + k];
+    if (tr) tr[o] = sb[ro + 5 * (int64_t)rows + k];
+  }
+}
+
 // ====================================================================== host side
 #include "pe_handle.hpp"
 
@@ -2364,6 +2526,8 @@ size_t lds_bytes(const Geo& g) {
 // (same-box A/B, profiles/r3b_ab_epb*.jsonl: 4096 envs 5.06 -> 4.55 us with 16-env
 // workgroups, 8192: 16 ~ 32, 16384: 32 best, 32768: 32 ~ 64)
 constexpr int kSmallBatch16 = 8192, kSmallBatch32 = 32768, kSmallBatch8W = 4096;
+// workgroups per CU of the persistent pipelined kernel (pe_pipe.hpp) above kSmallBatch32
+constexpr int kPipeWpc = 2;
 
 enum Variant {
   V_GENERIC = 0, V_C16R6_1W = 1, V_C16R6 = 2, V_C64R6 = 3,
@@ -2387,7 +2551,25 @@ size_t quad_lds_bytes(const Geo& g, bool codes) {
 
 bool is_quad(int v) { return v >= V_QUAD_C16R6_1W; }
 
+// the persistent pipelined kernel's grid and LDS: min(blocks, WPC per CU); the LDS
+// request caps residency at WPC workgroups per CU (the grid assumes it)
+int launch_pipe(const pe_handle* h, const StepArgs& a, hipStream_t s) {
+  const int wpc = h->pipe_wpc;
+  const int64_t nblk = ((int64_t)h->n + kQuadEnvs - 1) / kQuadEnvs;
+  dim3 grid((unsigned)std::min<int64_t>(nblk, (int64_t)wpc * h->num_cus)), block(256);
+  size_t lds = quad_lds_bytes(h->g, false);
+  if (wpc < 4) lds = std::max(lds, (size_t)160 * 1024 / (wpc + 1) + 16);
+  switch (wpc) {
+    case 2: hipLaunchKernelGGL((pe_step_pipe<16, 6, 2>), grid, block, lds, s, a); break;
+    case 3: hipLaunchKernelGGL((pe_step_pipe<16, 6, 3>), grid, block, lds, s, a); break;
+    default: hipLaunchKernelGGL((pe_step_pipe<16, 6, 4>), grid, block, lds, s, a); break;
+  }
+  PE_HIP(hipGetLastError());
+  return PE_OK;
+}
+
 int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
+  if (h->pipe_wpc > 0) return launch_pipe(h, a, s);
   if (is_quad(h->variant)) {
     const int nw = h->quad_waves, epb = h->quad_epb;
     dim3 grid((unsigned)((h->n + epb - 1) / epb)), block(nw * 64);
@@ -2714,7 +2896,6 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   // sector kernels of the other specialized geometries (4 waves; no lane-kernel twin)
   if (!lane_kernels && C == 10 && R == 2 && table_matches<10, 2>(ldx, ldy)) h->variant = V_QUAD_C10R2_1W;
   if (!lane_kernels && C == 16 && R == 4 && table_matches<16, 4>(ldx, ldy)) h->variant = V_QUAD_C16R4_1W;
-  if (h->variant >= V_QUAD_C10R2_1W) h->quad_waves = 4;
   // the one-word form (whole padded row in one u64) needs WPR == 1 and 16-B visit
   // rows (NW == 4: G <= 20); otherwise the multi-word (funnel-shifted) form
   const bool oneword = g.WPR == 1 && g.NW == 4;
@@ -2724,6 +2905,8 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   // workgroup share the per-env work the wave kernel repeats per wave
   if (!lane_kernels && h->variant == V_GENERIC && C >= 4 && C <= kRtCMax && R >= 2 && R <= kRtRMax)
     h->variant = oneword ? V_QUAD_RT_1W : V_QUAD_RT;
+  // the sector kernels of these geometries (and the runtime-(C, R) one) exist with 4 waves only
+  if (h->variant >= V_QUAD_C10R2_1W) h->quad_waves = 4;
   if (h->variant == V_QUAD_C16R6_1W && g.NW != 4) h->variant = V_C16R6_1W;  // needs 16-B visit rows
   // byte-coded obs tile where the f32 tile limits the sector kernel's occupancy
   // (C = 64: 89 KB -> 22 KB of LDS per workgroup)
@@ -2732,6 +2915,17 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   if (const char* tc = std::getenv("PE_TILE_CODES"))
     if (h->variant == V_QUAD_C16R6_1W || h->variant == V_QUAD_C64R6) h->tile_codes = std::atoi(tc) != 0;
 #endif
+  // obs as byte codes at the boundary (pe_step_codes): the byte-coded tile kernels
+  h->obs_codes = c->obs_codes ? 1 : 0;
+  if (h->obs_codes) {
+    if (!(h->variant == V_QUAD_C16R6_1W || h->variant == V_QUAD_C64R6)) {
+      delete[] ldx;
+      delete[] ldy;
+      delete h;
+      return fail(PE_ERR_ARG, "obs_codes needs a byte-coded sector kernel (C=16/R=6 with G<=20, or C=64/R=6)");
+    }
+    h->tile_codes = 1;
+  }
   if (h->tile_codes) {
     h->quad_waves = 4;
     // all 1024 workgroups of a 65536-env batch are resident at once (4 per CU) and
@@ -2750,6 +2944,12 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
     if (std::strcmp(kenv, "wave") == 0) h->variant = V_GENERIC;  // A/B: the one-wave-per-env kernel
 #endif
   if (!is_quad(h->variant)) h->tile_codes = 0;
+  if (h->obs_codes && !h->tile_codes) {
+    delete[] ldx;
+    delete[] ldy;
+    delete h;
+    return fail(PE_ERR_ARG, "obs_codes: the byte-coded tile does not fit this geometry");
+  }
   // envs per workgroup: a batch too small to give every CU four 64-env workgroups
   // (1024 at 65536 envs) is cut into 16- or 32-env workgroups instead, so that it
   // still spreads over all 256 CUs (headline geometry's kernel only; 4 waves, f32 tile)
@@ -2767,7 +2967,21 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
       h->quad_epb = v == 16 || (v == 32 && h->quad_waves == 4) ? v : kQuadEnvs;  // 8 waves: 16 or 64
     }
 #endif
+  // the persistent pipelined kernel (pe_pipe.hpp): the headline geometry's 64-env,
+  // 4-wave, f32-tile kernel at batches that fill the chip
+  h->num_cus = prop.multiProcessorCount;
+  h->pipe_wpc = n_envs > kSmallBatch32 ? kPipeWpc : 0;
+#ifdef PE_DEBUG_KNOBS
+  if (const char* pp = std::getenv("PE_PIPE")) h->pipe_wpc = std::min(std::max(std::atoi(pp), 0), 4);
+#endif
+  if (h->pipe_wpc == 1) h->pipe_wpc = 2;
+  if (!(h->variant == V_QUAD_C16R6_1W && h->quad_epb == kQuadEnvs && h->quad_waves == 4 && !h->tile_codes))
+    h->pipe_wpc = 0;
   h->kname = variant_name(h->variant);
+  if (h->pipe_wpc > 0) {
+    std::snprintf(h->kname_buf, sizeof(h->kname_buf), "pe_step_pipe<C16,R6,1word,P%d>", h->pipe_wpc);
+    h->kname = h->kname_buf;
+  }
   if (h->quad_epb != kQuadEnvs) {
     std::snprintf(h->kname_buf, sizeof(h->kname_buf), "%.*s%s,E%d>", (int)std::strlen(h->kname) - 1, h->kname,
                   h->quad_waves == 8 ? ",W8" : "", h->quad_epb);
@@ -3023,6 +3237,64 @@ int pe_step(pe_handle* h, const void* actions, int32_t action_bytes, float* obs,
   if (rc != PE_OK || h->pf_every <= 0 || ++h->pf_count < h->pf_every) return rc;
   h->pf_count = 0;
   return launch_prefetch(h, static_cast<hipStream_t>(stream), 0);  // maps for the envs reset since the last one
+}
+
+int pe_step_codes(pe_handle* h, const void* actions, int32_t action_bytes, uint8_t* obs_codes, float* reward,
+                  uint8_t* terminated, uint8_t* truncated, float* terminal_obs, double* ep_ret, int32_t* ep_len,
+                  int32_t* terminal_info, void* stream) {
+  if (!h || !actions || !obs_codes || !reward || !terminated || !truncated) return fail(PE_ERR_ARG, "null argument");
+  if (!h->obs_codes) return fail(PE_ERR_ARG, "pe_step_codes needs a handle created with obs_codes = 1");
+  if (action_bytes != 4 && action_bytes != 8) return fail(PE_ERR_ARG, "action_bytes must be 4 or 8");
+  DeviceGuard dg(h);
+  if (dg.rc) return dg.rc;
+  StepArgs a = base_args(h);
+  a.act_bytes = action_bytes;
+  a.actions = actions;
+  a.obs_codes = obs_codes;
+  a.reward = reward;
+  a.term = terminated;
+  a.trunc = truncated;
+  a.tobs = terminal_obs;
+  a.ep_ret_out = ep_ret;
+  a.ep_len_out = ep_len;
+  a.tinfo = terminal_info;
+  const int rc = launch_step(h, a, static_cast<hipStream_t>(stream));
+  if (rc != PE_OK || h->pf_every <= 0 || ++h->pf_count < h->pf_every) return rc;
+  h->pf_count = 0;
+  return launch_prefetch(h, static_cast<hipStream_t>(stream), 0);
+}
+
+int pe_obs_code_table(const pe_handle* h, float* table) {
+  if (!h || !table) return fail(PE_ERR_ARG, "null argument");
+  // obs_code_value on the host tables: the same f32 quotients pe_create uploads
+  const int R = h->g.R, G = h->g.G;
+  for (int c = 0; c < 256; ++c) {
+    float v = 0.0f;
+    if (c <= R) v = (float)((double)c / (double)R);
+    else if (c == R + 1) v = 1.0f;
+    else if (c >= kCodeVis && c < kCodeVis + 16) v = (float)((double)(c - kCodeVis < 10 ? c - kCodeVis : 10) / 10.0);
+    else if (c >= kCodePos && c < kCodePos + G) v = (float)((double)(c - kCodePos) / (double)G);
+    table[c] = v;
+  }
+  return PE_OK;
+}
+
+int pe_expand_obs_codes(const pe_handle* h, int32_t blocks, int32_t rows, const uint8_t* src, int64_t src_stride,
+                        float* obs, float* reward, uint8_t* terminated, uint8_t* truncated, void* stream) {
+  if (!h || !src || !obs) return fail(PE_ERR_ARG, "null argument");
+  if (blocks < 1 || blocks > 65535 || rows < 1) return fail(PE_ERR_ARG, "blocks must be 1..65535, rows >= 1");
+  const int64_t need = (((int64_t)rows * h->g.D + 15) & ~(int64_t)15) + 6 * (int64_t)rows;
+  if (blocks > 1 && (src_stride < need || (src_stride & 15))) return fail(PE_ERR_ARG, "src_stride too small or not a multiple of 16");
+  if ((reinterpret_cast<uintptr_t>(src) & 15u) || (reinterpret_cast<uintptr_t>(obs) & 15u))
+    return fail(PE_ERR_ARG, "src and obs must be 16-B aligned");
+  DeviceGuard dg(h);
+  if (dg.rc) return dg.rc;
+  const int64_t groups = ((int64_t)rows * h->g.D + 3) / 4;
+  dim3 grid((unsigned)((groups + 255) / 256), (unsigned)blocks), block(256);
+  hipLaunchKernelGGL(pe_expand_codes_kernel, grid, block, 0, static_cast<hipStream_t>(stream), h->st.tab, h->g.R,
+                     h->g.G, h->g.D, rows, src, src_stride, obs, reward, terminated, truncated);
+  PE_HIP(hipGetLastError());
+  return PE_OK;
 }
 
 int pe_get_info(pe_handle* h, int32_t* info, void* stream) {

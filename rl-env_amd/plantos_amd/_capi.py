@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(HERE, "libplantos_hip.so")
 if os.environ.get("PLANTOS_HIP_LIB"):
     LIB_PATH = os.environ["PLANTOS_HIP_LIB"]
 
-PE_ABI_VERSION = 3
+PE_ABI_VERSION = 4
 PE_OK, PE_ERR_ARG, PE_ERR_DEVICE, PE_ERR_NOMEM, PE_ERR_NOROOM = 0, -1, -2, -3, -4
 PE_NSCAL = 8
 PE_NINFO = 11
@@ -40,6 +40,7 @@ EXPORTS = [
     "pe_pystream_create", "pe_pystream_next", "pe_pystream_getrandbits32", "pe_pystream_destroy",
     "pe_curriculum_enable", "pe_curriculum_disable", "pe_curriculum_get",
     "pe_mcts_create", "pe_mcts_destroy", "pe_mcts_seed", "pe_mcts_set_rng", "pe_mcts_get_rng", "pe_mcts_search",
+    "pe_step_codes", "pe_obs_code_table", "pe_expand_obs_codes",
 ]
 
 
@@ -52,8 +53,8 @@ class PEConfig(ctypes.Structure):
         ("r_water_empty", ctypes.c_double), ("r_step", ctypes.c_double), ("r_exploration", ctypes.c_double),
         ("r_revisit", ctypes.c_double), ("r_complete", ctypes.c_double), ("seed", ctypes.c_uint64),
         ("env_id_offset", ctypes.c_uint32), ("map_generation_algo", ctypes.c_int32),
-        ("coop_max_done", ctypes.c_int32), ("prefetch_every", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 4),
+        ("coop_max_done", ctypes.c_int32), ("prefetch_every", ctypes.c_int32), ("obs_codes", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 3),
     ]
 
 
@@ -85,6 +86,9 @@ def lib():
     L.pe_seed.argtypes = [P, U64, I32, P]
     L.pe_reset.argtypes = [P, P, P, P]
     L.pe_step.argtypes = [P, P, I32, P, P, P, P, P, P, P, P, P]
+    L.pe_step_codes.argtypes = [P, P, I32, P, P, P, P, P, P, P, P, P]
+    L.pe_obs_code_table.argtypes = [P, P]
+    L.pe_expand_obs_codes.argtypes = [P, I32, I32, P, ctypes.c_int64, P, P, P, P, P]
     L.pe_get_info.argtypes = [P, P, P]
     L.pe_get_state.argtypes = [P, P, P, P, P, P]
     L.pe_set_state.argtypes = [P, P, P, P, P, P]
@@ -122,7 +126,8 @@ def lib():
                  "pe_set_state", "pe_load_maps", "pe_synth_actions", "pe_poll_errors", "pe_pystream_create",
                  "pe_pystream_next", "pe_pystream_destroy", "pe_curriculum_enable", "pe_curriculum_disable",
                  "pe_curriculum_get", "pe_mcts_create", "pe_mcts_destroy", "pe_mcts_seed", "pe_mcts_set_rng",
-                 "pe_mcts_get_rng", "pe_mcts_search"):
+                 "pe_mcts_get_rng", "pe_mcts_search", "pe_step_codes", "pe_obs_code_table",
+                 "pe_expand_obs_codes"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L

@@ -23,12 +23,19 @@ class PlantOSBatch:
     is the fork's ('original' or 'maze', gradio-app/plantos_env_new.py:28).
     `coop_max_done` / `prefetch_every` tune the auto-reset paths (pe_config; None =
     the library's choice); they change speed, never results.
+
+    `obs_codes=True` (pe_config.obs_codes; geometries with a byte-coded sector
+    kernel): the step writes the obs as byte codes (codes.py) -- the io buffer is
+    codes u8 [n, D] | reward | terminated | truncated, `step()` returns the codes in
+    place of the f32 obs, and `expand_codes` turns one or many such buffers (e.g.
+    every rank's, gathered) into f32 in one kernel.  The host-boundary form of a
+    sharded job (shard.py).
     """
 
     def __init__(self, num_envs, grid_size=21, num_plants=8, num_obstacles=50, lidar_range=2,
                  lidar_channels=10, thirsty_plant_prob=0.7, max_steps=1000, autoreset=True, seed=0,
                  env_id_offset=0, device=None, rewards=None, map_generation_algo="original",
-                 coop_max_done=None, prefetch_every=None):
+                 coop_max_done=None, prefetch_every=None, obs_codes=False):
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device() if torch.cuda.is_available() else 0)
         self.device = torch.device(device)
@@ -46,6 +53,8 @@ class PlantOSBatch:
             cfg.coop_max_done = int(coop_max_done)
         if prefetch_every is not None:
             cfg.prefetch_every = int(prefetch_every)
+        cfg.obs_codes = int(bool(obs_codes))
+        self.obs_codes = bool(obs_codes)
         self.map_generation_algo = "maze" if cfg.map_generation_algo == C.PE_MAP_MAZE else "original"
         for k, v in (rewards or {}).items():
             setattr(cfg, k, float(v))
@@ -65,7 +74,7 @@ class PlantOSBatch:
         # with one collective (shard.py).
         self._io = self.new_io()
         self.obs, self.reward, self.terminated, self.truncated = self.io_views(self._io)
-        self._packed = self._io[4 * n * D:]
+        self._packed = self._io[self._io_offsets()[0]:]
         self.terminal_obs = torch.zeros((n, D), dtype=torch.float32, device=dev)
         self.episode_return = torch.zeros(n, dtype=torch.float64, device=dev)
         self.episode_length = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -100,21 +109,56 @@ class PlantOSBatch:
 
     @property
     def io(self):
-        """u8 [4nD + 6n] device buffer of one step's outputs (see io_views)."""
+        """u8 device buffer of one step's outputs (see io_views)."""
         return self._io
 
+    def _io_offsets(self):
+        """(reward, terminated, truncated, total) byte offsets of the io buffer."""
+        n, D = self.num_envs, self.obs_dim
+        if self.obs_codes:
+            from .codes import io_layout
+            return io_layout(n, D)
+        return 4 * n * D, 4 * n * (D + 1), 4 * n * (D + 1) + n, 4 * n * (D + 1) + 2 * n
+
     def io_bytes(self):
-        return 4 * self.num_envs * self.obs_dim + 6 * self.num_envs
+        return self._io_offsets()[3]
 
     def new_io(self):
         """A fresh output buffer for step(io=...) (e.g. double buffering)."""
         return torch.zeros(self.io_bytes(), dtype=torch.uint8, device=self.device)
 
     def io_views(self, io):
-        """(obs f32 [n, D], reward f32 [n], terminated u8 [n], truncated u8 [n]) views of io."""
+        """(obs f32 [n, D] -- or codes u8 [n, D] with obs_codes --, reward f32 [n],
+        terminated u8 [n], truncated u8 [n]) views of io."""
         n, D = self.num_envs, self.obs_dim
-        return (io[:4 * n * D].view(torch.float32).view(n, D), io[4 * n * D:4 * n * (D + 1)].view(torch.float32),
-                io[4 * n * (D + 1):4 * n * (D + 1) + n], io[4 * n * (D + 1) + n:])
+        ro, to, tro, end = self._io_offsets()
+        obs = io[:n * D].view(n, D) if self.obs_codes else io[:ro].view(torch.float32).view(n, D)
+        return obs, io[ro:to].view(torch.float32), io[to:tro], io[tro:tro + n]
+
+    def code_table(self):
+        """float32[256] (host): the value of every obs byte code (pe_obs_code_table)."""
+        import numpy as np
+        t = np.zeros(256, np.float32)
+        C.check(C.lib().pe_obs_code_table(self.handle, t.ctypes.data_as(ctypes.c_void_p)), "pe_obs_code_table")
+        return t
+
+    def expand_codes(self, src, blocks=1, obs=None, reward=None, terminated=None, truncated=None):
+        """f32 obs (and, where given, reward / terminated / truncated) of `blocks` code-mode
+        io buffers of this batch's size laid out back to back in `src` (a contiguous u8
+        device tensor of blocks * io_bytes(), e.g. the root's gather buffer) -- one
+        kernel, written straight into the given (or new) contiguous tensors."""
+        n, D = self.num_envs, self.obs_dim
+        stride = self.io_bytes()
+        if not (type(src) is torch.Tensor and src.dtype is torch.uint8 and src.is_cuda and src.is_contiguous()
+                and src.numel() == blocks * stride):
+            raise ValueError(f"src must be a contiguous uint8 device tensor of {blocks} x {stride} bytes")
+        if obs is None:
+            obs = torch.empty((blocks * n, D), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            C.check(C.lib().pe_expand_obs_codes(self.handle, int(blocks), n, _ptr(src), stride, _ptr(obs), _ptr(reward),
+                                                _ptr(terminated), _ptr(truncated), self._stream()),
+                    "pe_expand_obs_codes")
+        return obs, reward, terminated, truncated
 
     @property
     def packed_outputs(self):
@@ -153,7 +197,10 @@ class PlantOSBatch:
 
     # ----------------------------------------------------------------- hot path
     def reset(self, mask=None, obs=None):
-        """Reset masked envs (all if mask is None); returns obs [n, D] (device)."""
+        """Reset masked envs (all if mask is None); returns obs [n, D] (device, f32;
+        with obs_codes a new f32 tensor unless `obs` is given)."""
+        if obs is None and self.obs_codes:
+            obs = torch.empty((self.num_envs, self.obs_dim), dtype=torch.float32, device=self.device)
         out = self.obs if obs is None else obs
         m = None
         if mask is not None:
@@ -175,12 +222,13 @@ class PlantOSBatch:
                 raise ValueError(f"io must be a contiguous uint8 tensor of {self.io_bytes()} bytes on {self.device} "
                                  "(PlantOSBatch.new_io())")
             o, r_, te_, tr_ = self.io_views(io)
-            rc = self._L.pe_step(self.handle, self._actions_ptr(actions), self._act_bytes, o.data_ptr(),
+            step = self._L.pe_step_codes if self.obs_codes else self._L.pe_step
+            rc = step(self.handle, self._actions_ptr(actions), self._act_bytes, o.data_ptr(),
                                  r_.data_ptr(), te_.data_ptr(), tr_.data_ptr(),
                                  self._tobs_ptr if want_terminal_obs else None, self._ep_ptrs[0], self._ep_ptrs[1],
                                  self._ep_ptrs[2], torch.cuda.current_stream(self._dev_index).cuda_stream)
             if rc:
-                C.check(rc, "pe_step")
+                C.check(rc, "pe_step_codes" if self.obs_codes else "pe_step")
             return o, r_, te_, tr_
         a = actions
         if not (type(a) is torch.Tensor and a.is_cuda and a.get_device() == self._dev_index
@@ -189,12 +237,15 @@ class PlantOSBatch:
         if a.numel() != self.num_envs:
             raise ValueError(f"expected {self.num_envs} actions, got {a.numel()}")
         out = self.obs if obs is None else obs
+        if self.obs_codes and obs is not None:
+            raise ValueError("obs_codes: the step writes codes into the io buffer (expand_codes for f32)")
         r, te, tr = self._out_ptrs
-        rc = self._L.pe_step(self.handle, a.data_ptr(), a.element_size(), out.data_ptr(), r, te, tr,
+        step = self._L.pe_step_codes if self.obs_codes else self._L.pe_step
+        rc = step(self.handle, a.data_ptr(), a.element_size(), out.data_ptr(), r, te, tr,
                              self._tobs_ptr if want_terminal_obs else None, self._ep_ptrs[0], self._ep_ptrs[1],
                              self._ep_ptrs[2], torch.cuda.current_stream(self._dev_index).cuda_stream)
         if rc:
-            C.check(rc, "pe_step")
+            C.check(rc, "pe_step_codes" if self.obs_codes else "pe_step")
         return out, self.reward, self.terminated, self.truncated
 
     def _actions_ptr(self, actions):

@@ -9,6 +9,13 @@ batch: ``gather_outputs`` moves (obs, reward, terminated, truncated) to the root
 as ONE packed buffer per rank (RCCL ``gather`` over xGMI on GPUs; gloo on CPU in
 the tests; ``step_gather`` pipelines it behind the next step) and
 ``scatter_actions`` hands the root's actions back to the shards.
+
+``codes=True`` (the geometries with a byte-coded sector kernel, e.g. BASELINE config
+5's 20x20 / 16 rays): every rank's step writes its obs as byte codes (codes.py,
+pe_step_codes), so each rank contributes 5C+27 bytes of obs per env instead of
+4(5C+27) (7.1 MB instead of 28.4 MB per rank at 65536 envs), and the root expands
+all ranks' codes in ONE kernel straight into contiguous f32 [W*n, D] / reward /
+terminated / truncated tensors (``unpack``; no concatenation copy).
 """
 import torch
 import torch.distributed as dist
@@ -26,8 +33,9 @@ class ShardedPlantOS:
     (PlantOSBatch on the rank's GPU by default).
     """
 
-    def __init__(self, envs_per_rank, seed=0, batch_factory=None, group=None, **cfg):
+    def __init__(self, envs_per_rank, seed=0, batch_factory=None, group=None, codes=False, **cfg):
         self.group = group
+        self.codes = bool(codes)
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         # the collectives run whenever a process group exists -- also with one rank (a
@@ -39,9 +47,12 @@ class ShardedPlantOS:
             from .batch import PlantOSBatch
             dev = torch.device("cuda", torch.cuda.current_device())
             batch_factory = lambda n, **kw: PlantOSBatch(n, device=dev, **cfg, **kw)  # noqa: E731
-        self.batch = batch_factory(self.n, env_id_offset=lo, seed=seed)
+        extra = {"obs_codes": True} if self.codes else {}
+        self.batch = batch_factory(self.n, env_id_offset=lo, seed=seed, **extra)
         self._slots = None
         self._last_io = None  # the buffer the latest step wrote (None: the batch's own io)
+        self._gbuf = None     # root: gather_outputs' [W, io_bytes] buffer
+        self._out = None      # root, codes: the expanded global outputs (reused every step)
 
     @property
     def device(self):
@@ -53,7 +64,12 @@ class ShardedPlantOS:
 
     def io_bytes(self):
         """Bytes of one rank's packed step outputs (what one gather moves per rank)."""
-        return 4 * self.n * self.batch.obs_dim + 6 * self.n
+        return self.batch.io_bytes()
+
+    def _gather_buffer(self):
+        """Root: one contiguous [W, io_bytes] buffer the W ranks' buffers are gathered
+        into (its rows are the gather list: no copy to assemble it afterwards)."""
+        return torch.empty((self.world, self.io_bytes()), dtype=torch.uint8, device=self.device)
 
     def _pack(self):
         """The latest step's outputs of this shard as ONE flat u8 buffer: the buffer
@@ -67,11 +83,27 @@ class ShardedPlantOS:
         return torch.cat([t.contiguous().view(-1).view(torch.uint8)
                           for t in (b.obs, b.reward, b.terminated, b.truncated)])
 
-    def unpack(self, flats):
-        """The W ranks' packed buffers (rank order, e.g. ``gathered(slot)``) as the
-        global (obs f32 [W*n, D], reward f32 [W*n], terminated u8, truncated u8)."""
+    def unpack(self, flats, out=None):
+        """The W ranks' packed buffers (rank order: ``gathered(slot)``'s [W, io_bytes]
+        rows) as the global (obs f32 [W*n, D], reward f32 [W*n], terminated u8,
+        truncated u8).  codes: ONE expansion kernel writes them into `out` (four
+        contiguous tensors; default: buffers this object owns and reuses, valid until
+        the next unpack); otherwise the f32 parts are concatenated."""
         n = self.n
         D = self.batch.obs_dim
+        if self.codes:
+            src = flats if isinstance(flats, torch.Tensor) else torch.stack(list(flats))
+            W = src.shape[0] if src.dim() == 2 else 1
+            if out is None:
+                if self._out is None or self._out[0].shape[0] != W * n:
+                    dev = src.device
+                    self._out = (torch.empty((W * n, D), dtype=torch.float32, device=dev),
+                                 torch.empty(W * n, dtype=torch.float32, device=dev),
+                                 torch.empty(W * n, dtype=torch.uint8, device=dev),
+                                 torch.empty(W * n, dtype=torch.uint8, device=dev))
+                out = self._out
+            self.batch.expand_codes(src.reshape(-1), W, *out)
+            return out
         sizes = (4 * n * D, 4 * n, n, n)
         parts = [[], [], [], []]
         for f in flats:
@@ -88,12 +120,16 @@ class ShardedPlantOS:
         output buffer (RCCL over xGMI on GPUs)."""
         flat = self._pack()
         if not self._coll:
-            return self.unpack([flat])
-        lst = [torch.empty_like(flat) for _ in range(self.world)] if self.rank == root else None
+            return self.unpack(flat.view(1, -1))
+        lst = None
+        if self.rank == root:
+            if self._gbuf is None:
+                self._gbuf = self._gather_buffer()
+            lst = list(self._gbuf)
         dist.gather(flat, lst, dst=root, group=self.group)
         if self.rank != root:
             return None
-        return self.unpack(lst)
+        return self.unpack(self._gbuf)
 
     def step_gather(self, actions_local, root=0):
         """Pipelined step + host-boundary gather (GPU batches): the step writes into
@@ -107,8 +143,7 @@ class ShardedPlantOS:
         b = self.batch
         if self._slots is None:
             self._slots = [b.new_io(), b.new_io()]
-            self._glist = [[torch.empty_like(self._slots[k]) for _ in range(self.world)]
-                           if (self.rank == root and self._coll) else None for k in range(2)]
+            self._glist = [self._gather_buffer() if (self.rank == root and self._coll) else None for k in range(2)]
             self._work = [None, None]
             self._root = root
             self._k = 0
@@ -120,15 +155,18 @@ class ShardedPlantOS:
         b.step(actions_local, io=self._slots[k])
         self._last_io = self._slots[k]
         if self._coll:
-            self._work[k] = dist.gather(self._slots[k], self._glist[k], dst=root, group=self.group, async_op=True)
+            lst = list(self._glist[k]) if self._glist[k] is not None else None
+            self._work[k] = dist.gather(self._slots[k], lst, dst=root, group=self.group, async_op=True)
         return k
 
     def gathered(self, k):
-        """Root: the W ranks' packed buffers of slot k (rank order); None elsewhere."""
+        """Root: the W ranks' packed buffers of slot k as the rows of one [W, io_bytes]
+        tensor (rank order); None elsewhere.  Without a process group: slot k itself
+        as a [1, io_bytes] view."""
         if self._slots is None:
             raise ValueError("no step_gather yet")
         if not self._coll:
-            return [self._slots[k]]
+            return self._slots[k].view(1, -1)
         return self._glist[k]
 
     def wait(self, k):

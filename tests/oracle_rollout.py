@@ -47,9 +47,10 @@ class OracleBatch:
     lets the host-side vec-env logic run and be checked without a GPU)."""
 
     def __init__(self, n, grid_size, num_plants, num_obstacles, lidar_range, lidar_channels, seed=0,
-                 max_steps=1000):
+                 max_steps=1000, obs_codes=False):
         import torch
         self.torch = torch
+        self.obs_codes = bool(obs_codes)  # io holds byte codes (plantos_amd/codes.py), as PlantOSBatch's
         self.device = torch.device("cpu")
         self.num_envs = n
         self.grid_size = grid_size
@@ -85,30 +86,59 @@ class OracleBatch:
         self.obs = self.torch.as_tensor(self.ov.obs())
         return self.obs
 
-    # PlantOSBatch's packed output buffer: obs f32 [n, D] | reward f32 | term u8 | trunc u8
+    # PlantOSBatch's packed output buffer: obs f32 [n, D] (or codes u8 [n, D]) | reward f32 |
+    # term u8 | trunc u8
+    def _io_offsets(self):
+        n, D = self.num_envs, self.obs_dim
+        if self.obs_codes:
+            from plantos_amd.codes import io_layout
+            return io_layout(n, D)
+        return 4 * n * D, 4 * n * (D + 1), 4 * n * (D + 1) + n, 4 * n * (D + 1) + 2 * n
+
     def io_bytes(self):
-        return 4 * self.num_envs * self.obs_dim + 6 * self.num_envs
+        return self._io_offsets()[3]
 
     def new_io(self):
         return self.torch.zeros(self.io_bytes(), dtype=self.torch.uint8)
 
     def io_views(self, io):
         n, D = self.num_envs, self.obs_dim
-        f32 = self.torch.float32
-        return (io[:4 * n * D].view(f32).view(n, D), io[4 * n * D:4 * n * (D + 1)].view(f32),
-                io[4 * n * (D + 1):4 * n * (D + 1) + n], io[4 * n * (D + 1) + n:])
+        ro, to, tro, _ = self._io_offsets()
+        obs = io[:n * D].view(n, D) if self.obs_codes else io[:ro].view(self.torch.float32).view(n, D)
+        return obs, io[ro:to].view(self.torch.float32), io[to:tro], io[tro:tro + n]
+
+    def _io_values(self, outs):
+        """the step's outputs as the io holds them (obs encoded in code mode)"""
+        if not self.obs_codes:
+            return outs
+        from plantos_amd.codes import encode_obs
+        G, _, _, R, C = self.cfg_t
+        return (self.torch.as_tensor(encode_obs(outs[0].numpy(), G, C, R)),) + tuple(outs[1:])
 
     @property
     def io(self):
         io = self.new_io()
-        for dst, src in zip(self.io_views(io), (self.obs, self.reward, self.terminated, self.truncated)):
+        for dst, src in zip(self.io_views(io), self._io_values((self.obs, self.reward, self.terminated,
+                                                                self.truncated))):
             dst.copy_(src)
         return io
+
+    def expand_codes(self, src, blocks=1, obs=None, reward=None, terminated=None, truncated=None):
+        """host twin of PlantOSBatch.expand_codes (plantos_amd/codes.py expand_host)"""
+        from plantos_amd.codes import code_table, expand_host
+        G, _, _, R, _ = self.cfg_t
+        n, D = self.num_envs, self.obs_dim
+        if obs is None:
+            obs = self.torch.empty((blocks * n, D), dtype=self.torch.float32)
+        expand_host(src.numpy(), blocks, n, D, self.io_bytes(), code_table(G, R), obs.numpy(),
+                    None if reward is None else reward.numpy(), None if terminated is None else terminated.numpy(),
+                    None if truncated is None else truncated.numpy())
+        return obs, reward, terminated, truncated
 
     def step(self, actions, io=None):
         if io is not None:
             outs = self.step(actions)
-            for dst, src in zip(self.io_views(io), outs):
+            for dst, src in zip(self.io_views(io), self._io_values(outs)):
                 dst.copy_(src)
             return self.io_views(io)
         a = np.asarray(actions.cpu().numpy() if hasattr(actions, "cpu") else actions, np.int64)

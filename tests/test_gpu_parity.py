@@ -162,14 +162,18 @@ def test_kernel_selection(name):
     b.close()
 
 
+# the headline geometry above 32768 envs: the persistent pipelined kernel (pe_pipe.hpp)
+PIPE_KERNEL = "pe_step_pipe<C16,R6,1word,P2>"
+
+
 @pytest.mark.parametrize("n,suffix", [(1, ",W8,E16"), (4096, ",W8,E16"), (4097, ",E16"), (8192, ",E16"),
-                                      (8193, ",E32"), (32768, ",E32"), (32769, ""), (65536, "")])
+                                      (8193, ",E32"), (32768, ",E32"), (32769, None), (65536, None)])
 def test_small_batch_workgroup_shape(n, suffix):
     """Batches too small for four 64-env workgroups per CU run 16- or 32-env
-    workgroups of the same kernel, up to 4096 envs with 8 waves (sectors of 2 rays)
-    -- pe_create's choice, by batch size"""
+    workgroups of the same kernel, up to 4096 envs with 8 waves (sectors of 2 rays);
+    larger ones the persistent pipelined kernel -- pe_create's choice, by batch size"""
     b = make(CFG["g20"], n)
-    assert b.kernel_name == "pe_step_quad<C16,R6,1word" + suffix + ">"
+    assert b.kernel_name == (PIPE_KERNEL if suffix is None else "pe_step_quad<C16,R6,1word" + suffix + ">")
     b.close()
 
 
