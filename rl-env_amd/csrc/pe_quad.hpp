@@ -170,6 +170,13 @@ __device__ __forceinline__ void quad_rays_rt(const uint64_t* lrow, const int16_t
       row[5 * i + 2] = ov.y;
       row[5 * i + 3] = ov.z;
       row[5 * i + 4] = ov.w;
+    } else {  // byte codes (pe_coop.hpp ObsW<uint8_t>), as quad_rays
+      row[5 * i] = (uint8_t)((f >> 1) + 1);  // code r = dist[r] (R+1: 1.0, nothing hit)
+      const uint32_t oh = (uint32_t)(R + 1) << (8 * ent);  // one-hot as codes {0, R+1}
+      row[5 * i + 1] = (uint8_t)oh;
+      row[5 * i + 2] = (uint8_t)(oh >> 8);
+      row[5 * i + 3] = (uint8_t)(oh >> 16);
+      row[5 * i + 4] = (uint8_t)(oh >> 24);
     }
   }
 }

@@ -613,8 +613,10 @@ template <int R>
 constexpr int quad_tile_off() {
   return (kTabFloats + (2 * R + 3) * kQuadEnvs * 2 + 7 * kQuadEnvs + 3) & ~3;
 }
-// the runtime sector kernel (pe_step_quad<0, 0, ...>): maxima and its layout
-constexpr int kRtCMax = 32, kRtRMax = 14;
+// the runtime sector kernel (pe_step_quad<0, 0, ...>): maxima and its layout -- C up to
+// 32 with the f32 tile, up to 64 with the byte-coded one (the f32 tile of 64 rays holds
+// the kernel to one workgroup per CU)
+constexpr int kRtCMax = 32, kRtCMaxBT = 64, kRtRMax = 14;
 __host__ __device__ constexpr int quad_tile_off_rt(int R) {
   return (kTabFloats + (2 * R + 3) * kQuadEnvs * 2 + 7 * kQuadEnvs + 3) & ~3;
 }
@@ -622,6 +624,9 @@ __host__ __device__ constexpr int quad_tile_off_rt(int R) {
 template <int R, int C>
 constexpr int quad_ctab_off() {
   return quad_tile_off<R>() + ((kQuadEnvs * (5 * C + 27) + 15) / 16) * 4;
+}
+__host__ __device__ constexpr int quad_ctab_off_rt(int R, int C) {
+  return quad_tile_off_rt(R) + ((kQuadEnvs * (5 * C + 27) + 15) / 16) * 4;
 }
 
 // ---- pe_step_quad's auto-reset slow path (a block with a done env), out of line:
@@ -1182,10 +1187,11 @@ __device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* 
 template <int C, int R, bool ONEWORD, int NW, bool BT = false, int EPB = kQuadEnvs>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs (small-batch EPB: one workgroup per CU, no cap); NW=4: <= 128 VGPRs (4 workgroups per CU: G=25 13.1 -> 10.5 us; 1-word C16: 122 -> 104 VGPRs)
   // C == 0 (R == 0): the runtime-(C, R) sector kernel (quad_rays_rt): C, R from the
-  // geometry (up to kRtCMax / kRtRMax), the LDS layout sized at run time
+  // geometry (up to kRtCMax -- kRtCMaxBT with the byte-coded tile -- / kRtRMax), the LDS
+  // layout sized at run time
   constexpr bool RT = C == 0;
-  constexpr int CM = RT ? kRtCMax : C, RM = RT ? kRtRMax : R;
-  static_assert(!RT || (R == 0 && !BT && NW == 4 && EPB == kQuadEnvs), "runtime sector kernel: 4 waves, f32 tile");
+  constexpr int CM = RT ? (BT ? kRtCMaxBT : kRtCMax) : C, RM = RT ? kRtRMax : R;
+  static_assert(!RT || (R == 0 && NW == 4 && EPB == kQuadEnvs), "runtime sector kernel: 4 waves, 64 envs");
   const int Cr = RT ? a.g.C : C, Rr = RT ? a.g.R : R;
   constexpr int NR = 2 * RM + 3, NV = 7, LS = kQuadEnvs, CW = NW - 1;  // CW: commit wave
   const int NRL = RT ? 2 * Rr + 3 : NR;  // window rows (the LDS layout's)
@@ -1204,7 +1210,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   uint32_t* lvis = reinterpret_cast<uint32_t*>(lrow + NRL * LS);   // [NV][LS]
   using OT = typename std::conditional<BT, uint8_t, float>::type;
   OT* rows = reinterpret_cast<OT*>(smem + tile_off);                // [LS][D] floats or codes
-  float* ctab = smem + quad_ctab_off<RM, CM>();                     // BT: code -> float
+  float* ctab = smem + (RT ? quad_ctab_off_rt(Rr, Cr) : quad_ctab_off<RM, CM>());  // BT: code -> float
   const Geo& g = a.g;
   const Rules& rl = a.rl;
   const State& st = a.st;
@@ -1261,7 +1267,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   if (threadIdx.x < 16) smem[kOneHotF + threadIdx.x] = (threadIdx.x >> 2) == (threadIdx.x & 3) ? 1.0f : 0.0f;
   if (threadIdx.x == 16) smem[Rr + 1] = 1.0f;
   if constexpr (BT) {
-    if (threadIdx.x < 256) ctab[threadIdx.x] = obs_code_value(st.tab, R, g.G, (int)threadIdx.x);
+    if (threadIdx.x < 256) ctab[threadIdx.x] = obs_code_value(st.tab, Rr, g.G, (int)threadIdx.x);
   }
   Scal s = unpack(sw);
 #ifdef PE_STAMPS
@@ -1280,7 +1286,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // only (64x64 desynchronized: 36.6 -> 36.2 us): at 20x20 the waits hipcc places
   // around a possibly outstanding LDS-DMA (a vmcnt(0) at the next use of any load
   // result) serialize round 2 in every block (9.39 -> 10.0 us, desync 11.52 -> 12.29).
-  float* stage = smem + (BT ? quad_ctab_off<RM, CM>() + 256 : tile_off + LS * (5 * Cr + 27));
+  float* stage = smem + (BT ? (RT ? quad_ctab_off_rt(Rr, Cr) : quad_ctab_off<RM, CM>()) + 256
+                            : tile_off + LS * (5 * Cr + 27));
   const bool stage_ok = BT && a.pf.scal && quad_coop(a, 1) && e0 + EPB <= a.n;  // full block: every lane live
   const bool stage_info = !st.cur && a.tinfo && pf_stage_info_fits(g.G, g.WPR, (int)a.pf.ostride);
   // (issued right after round 2's own loads: hipcc drains every memory op in flight
@@ -2534,7 +2541,7 @@ enum Variant {
   V_QUAD_C16R6_1W = 4, V_QUAD_C16R6 = 5, V_QUAD_C64R6 = 6,
   V_QUAD_C10R2_1W = 7, V_QUAD_C10R2 = 8,  // plantos_env.py:25-26 constructor default (G=21: multi-word)
   V_QUAD_C16R4_1W = 9, V_QUAD_C16R4 = 10,  // test_environment.py:24 (G=15, C=16, R=4)
-  V_QUAD_RT_1W = 11, V_QUAD_RT = 12        // runtime (C, R): every other geometry with C <= 32, 2 <= R <= 14
+  V_QUAD_RT_1W = 11, V_QUAD_RT = 12        // runtime (C, R): every other geometry with C <= 64, 2 <= R <= 14
 };
 
 // the prefetched records' obs row stride (bytes; pe_device.hpp Prefetch)
@@ -2599,8 +2606,18 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
       case V_QUAD_C10R2_1W: PE_QUAD4(10, 2, true); break;
       case V_QUAD_C10R2: PE_QUAD4(10, 2, false); break;
       case V_QUAD_C16R4_1W: PE_QUAD4(16, 4, true); break;
-      case V_QUAD_RT_1W: PE_QUAD4(0, 0, true); break;
-      case V_QUAD_RT: PE_QUAD4(0, 0, false); break;
+      case V_QUAD_RT_1W:
+        if (h->tile_codes)
+          hipLaunchKernelGGL((pe_step_quad<0, 0, true, 4, true>), grid, block, lds, s, a);
+        else
+          PE_QUAD4(0, 0, true);
+        break;
+      case V_QUAD_RT:
+        if (h->tile_codes)
+          hipLaunchKernelGGL((pe_step_quad<0, 0, false, 4, true>), grid, block, lds, s, a);
+        else
+          PE_QUAD4(0, 0, false);
+        break;
       default: PE_QUAD4(16, 4, false); break;
     }
 #undef PE_QUAD
@@ -2903,14 +2920,16 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   // every other geometry with 4 <= C <= 32 and 2 <= R <= 14: the sector kernel with
   // table-driven rays (quad_rays_rt) instead of one wave per env -- 64 envs per
   // workgroup share the per-env work the wave kernel repeats per wave
-  if (!lane_kernels && h->variant == V_GENERIC && C >= 4 && C <= kRtCMax && R >= 2 && R <= kRtRMax)
+  // (33 <= C <= 64: with the byte-coded tile, below)
+  if (!lane_kernels && h->variant == V_GENERIC && C >= 4 && C <= kRtCMaxBT && R >= 2 && R <= kRtRMax)
     h->variant = oneword ? V_QUAD_RT_1W : V_QUAD_RT;
   // the sector kernels of these geometries (and the runtime-(C, R) one) exist with 4 waves only
   if (h->variant >= V_QUAD_C10R2_1W) h->quad_waves = 4;
   if (h->variant == V_QUAD_C16R6_1W && g.NW != 4) h->variant = V_C16R6_1W;  // needs 16-B visit rows
   // byte-coded obs tile where the f32 tile limits the sector kernel's occupancy
   // (C = 64: 89 KB -> 22 KB of LDS per workgroup)
-  h->tile_codes = h->variant == V_QUAD_C64R6 ? 1 : 0;
+  h->tile_codes = h->variant == V_QUAD_C64R6 || (is_quad(h->variant) && h->variant >= V_QUAD_RT_1W && C > kRtCMax)
+                      ? 1 : 0;
 #ifdef PE_DEBUG_KNOBS
   if (const char* tc = std::getenv("PE_TILE_CODES"))
     if (h->variant == V_QUAD_C16R6_1W || h->variant == V_QUAD_C64R6) h->tile_codes = std::atoi(tc) != 0;
@@ -2918,11 +2937,13 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   // obs as byte codes at the boundary (pe_step_codes): the byte-coded tile kernels
   h->obs_codes = c->obs_codes ? 1 : 0;
   if (h->obs_codes) {
-    if (!(h->variant == V_QUAD_C16R6_1W || h->variant == V_QUAD_C64R6)) {
+    if (!(h->variant == V_QUAD_C16R6_1W || h->variant == V_QUAD_C64R6 || h->variant == V_QUAD_RT_1W ||
+          h->variant == V_QUAD_RT)) {
       delete[] ldx;
       delete[] ldy;
       delete h;
-      return fail(PE_ERR_ARG, "obs_codes needs a byte-coded sector kernel (C=16/R=6 with G<=20, or C=64/R=6)");
+      return fail(PE_ERR_ARG, "obs_codes needs a byte-coded sector kernel (C=16/R=6 with G<=20, C=64/R=6, or "
+                              "4<=C<=64 with 2<=R<=14 and no compile-time kernel)");
     }
     h->tile_codes = 1;
   }

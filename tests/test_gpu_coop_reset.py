@@ -26,7 +26,8 @@ CFG = {
     "g12r2": (12, 4, 6, 2, 10),   # one-word C10R2
     "g64r32": (64, 100, 120, 32, 64),  # the one-wave-per-env kernel (long rays)
     "g30r2": (30, 12, 40, 2, 10),  # multi-word C10R2
-    "g16c40": (16, 6, 8, 5, 40),   # C > 32: the one-wave-per-env kernel
+    "g16c40": (16, 6, 8, 5, 40),   # C > 32: the runtime sector kernel, byte-coded tile
+    "g40c48": (40, 100, 120, 8, 48),  # the same, multi-word rows (bench geometry)
 }
 
 
@@ -54,6 +55,8 @@ def info_rows(b, idx):
     ("g12r2", 600, 80, 60, None, None, None, None, False),
     ("g30r2", 400, 60, 50, None, None, None, None, False),
     ("g16c40", 300, 60, 50, None, None, None, None, False),
+    ("g40c48", 256, 60, 50, None, None, None, None, False),
+    ("g40c48", 128, 12, 1, "64", None, None, None, False),    # every env at once, cooperative, byte-coded records
     ("g64r32", 192, 50, 40, None, None, None, None, False),
     ("g64r32", 128, 12, 1, "0", None, None, None, False),    # dense: serial resets (coop_max_done 0)
     ("g21", 256, 12, 1, "0", None, None, None, False),        # the constructor default, dense: lane-per-env path

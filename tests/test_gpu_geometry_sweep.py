@@ -1,9 +1,12 @@
 """A seeded sweep of geometries through every step kernel the library selects: the
-runtime-(C, R) sector kernel (4 <= C <= 32, 2 <= R <= 14, one-word and multi-word
-rows), the compile-time sector kernels, and the one-wave-per-env kernel (C > 32 or
-R > 14) -- each against the oracle (plantos_env.py:160-315 restated), every output
-of every step, episodes desynchronized so that auto-resets happen inside the window,
-the final state included.  Batch sizes are ragged (a partial last workgroup)."""
+runtime-(C, R) sector kernel (4 <= C <= 64, 2 <= R <= 14, one-word and multi-word
+rows; a byte-coded obs tile above 32 rays), the compile-time sector kernels, and the
+one-wave-per-env kernel (C > 64, R > 14 or R = 1) -- each against the oracle
+(plantos_env.py:160-315 restated), every output of every step, episodes
+desynchronized so that auto-resets happen inside the window, the final state
+included.  Batch sizes are ragged (a partial last workgroup).  A second sweep covers
+33 <= C <= 64 (round 4: the byte-coded runtime sector kernel) and the byte-coded
+obs boundary (obs_codes) on runtime-sector geometries."""
 import numpy as np
 import pytest
 import torch
@@ -37,21 +40,56 @@ def _geometries():
     return out
 
 
+def _wide_geometries():
+    """33 <= C <= 64, 2 <= R <= 14 (the byte-coded runtime sector kernel)"""
+    rng = np.random.default_rng(4044)
+    out = []
+    while len(out) < 10:
+        C, R = int(rng.integers(33, 65)), int(rng.integers(2, 15))
+        G = int(rng.integers(5, 49))
+        cells = G * G
+        O_ = int(rng.integers(0, max(1, cells // 10)))
+        P = int(rng.integers(1, max(2, min(40, cells // 8))))
+        if (O_ // 3) * 9 + P + 1 > cells - 4 * G:
+            continue
+        out.append((G, P, O_, R, C))
+    return out
+
+
 GEOS = _geometries()
+WIDE = _wide_geometries()
 
 
-@pytest.mark.parametrize("cfg", GEOS, ids=[f"G{g}P{p}O{o}R{r}C{c}" for g, p, o, r, c in GEOS])
+def _ids(geos):
+    return [f"G{g}P{p}O{o}R{r}C{c}" for g, p, o, r, c in geos]
+
+
+@pytest.mark.parametrize("cfg", GEOS + WIDE, ids=_ids(GEOS) + _ids(WIDE))
 def test_geometry_sweep_parity(cfg):
+    _sweep(cfg, codes=False)
+
+
+# the byte-coded obs boundary on runtime-sector geometries (f32 and byte tiles)
+CODES = [g for g in GEOS if 4 <= g[4] <= 64 and 2 <= g[3] <= 14][:3] + WIDE[:3]
+
+
+@pytest.mark.parametrize("cfg", CODES, ids=_ids(CODES))
+def test_geometry_sweep_codes_parity(cfg):
+    _sweep(cfg, codes=True)
+
+
+def _sweep(cfg, codes):
     from plantos_amd import PlantOSBatch
     G, P, O_, R, C = cfg
     n, steps, seed = 133, 60, 17
     b = PlantOSBatch(n, grid_size=G, num_plants=P, num_obstacles=O_, lidar_range=R, lidar_channels=C, seed=seed,
-                     device="cuda:0")
-    rt = 4 <= C <= 32 and 2 <= R <= 14
+                     device="cuda:0", obs_codes=codes)
+    rt = 4 <= C <= 64 and 2 <= R <= 14
     if rt:  # (or a compile-time specialization of the same sector kernel)
         assert b.kernel_name.startswith("pe_step_quad"), b.kernel_name
-    elif C > 32 or R > 14:
+    elif C > 64 or R > 14:
         assert b.kernel_name == "pe_step_wave", b.kernel_name
+    f32 = torch.empty((n, b.obs_dim), dtype=torch.float32, device="cuda:0")
     ov = OracleVec(cfg, np.arange(n), seed)
     start = (999 - np.random.default_rng(3).integers(0, 40, n)).astype(np.int32)
     sc = b.get_state(parts=("scalars",))["scalars"].cpu().numpy()
@@ -62,6 +100,8 @@ def test_geometry_sweep_parity(cfg):
     for t in range(steps):
         b.synth_actions(seed, t, out=act)
         obs, rew, te, tr = b.step(act)
+        if codes:
+            obs = b.expand_codes(b.io, 1, f32)[0]
         o_obs, o_rew, o_te, o_tr, o_tobs, o_ret, o_len = ov.step(act.cpu().numpy())
         assert (rew.cpu().numpy() == o_rew.astype(np.float32)).all(), t
         assert (te.cpu().numpy().astype(bool) == o_te).all() and (tr.cpu().numpy().astype(bool) == o_tr).all(), t

@@ -27,7 +27,7 @@ CFG = {
     "g30r2": (30, 12, 40, 2, 10),  # multi-word C10R2 (G + 2R > 32)
     "g8r12": (8, 3, 3, 12, 16),    # R > G: runtime sector kernel, window rows mostly off the map
     "g8r20": (8, 3, 3, 20, 16),    # R > 14 and > G: the wave kernel's raw-window ray path (no rover-aligned re-staging)
-    "g16c40": (16, 6, 8, 5, 40),   # C > 32: the wave kernel (rover-aligned window)
+    "g16c40": (16, 6, 8, 5, 40),   # C > 32: the runtime sector kernel with the byte-coded tile
     "g24c100": (24, 10, 12, 8, 100),  # C = 100 (near the 120-ray LDS bound): wave kernel, rays past lane 63
 }
 
@@ -38,7 +38,7 @@ KERNELS = {
     "g21": "pe_step_quad<C10,R2>", "g12r2": "pe_step_quad<C10,R2,1word>", "g30r2": "pe_step_quad<C10,R2>", "g15": "pe_step_quad<C16,R4,1word>",
     "g25r4": "pe_step_quad<C16,R4>", "g64r32": "pe_step_wave", "g7": "pe_step_quad<runtime C,R,1word>",
     "g32": "pe_step_quad<runtime C,R>", "g8r12": "pe_step_quad<runtime C,R,1word>", "g24c100": "pe_step_wave",
-    "g8r20": "pe_step_wave", "g16c40": "pe_step_wave",
+    "g8r20": "pe_step_wave", "g16c40": "pe_step_quad<runtime C,R,1word>",
 }
 
 
