@@ -641,13 +641,32 @@ __device__ __forceinline__ bool coop_take_prefetched(const Prefetch& pf, const G
 }
 
 // The state writes of reset() for env e by one wave, given its new map (rows in
-// the lanes' registers) and scalars s: grid rows and visit rows to HBM (lane r
-// writes row r), the curriculum's carried-visits mode as new_episode_visits.
+// the lanes' registers) and scalars s: grid rows and visit rows (the new episode's
+// slot) to HBM (lane r writes row r), the curriculum's carried-visits mode as
+// new_episode_visits.
 // keep: CurriculumWrapper keeps the previous visit counts.
+// Fresh visit rows of a new episode (all zero, pads 10, visit[rover] = 1,
+// plantos_env.py:146-147) into its slot, lane r writing row r.
+__device__ inline void coop_fresh_visits(const State& st, const Geo& g, int64_t e, const Scal& s, int lane,
+                                         const Tables* tab) {
+  if (lane < g.G) {
+    uint32_t* vb = vis_env(st, g, e, s.episode) + (int64_t)lane * g.NW;
+    const int bit = 4 * (s.y + 2);
+    const bool rover = lane == s.x && !(s.flags & F_NOROOM);
+    for (int w = 0; w < g.NW; ++w) {
+      uint32_t v = (tab ? tab : st.tab)->vis_pad[w];
+      if (rover && w == (bit >> 5)) v = (v & ~(0xFu << (bit & 31))) | (1u << (bit & 31));
+      vb[w] = v;
+    }
+  }
+}
+
+// taken: s is a prefetched record's, whose fresh visit rows the prefetch kernel already
+// wrote into the new episode's slot (pe_device.hpp vis_env): no visit row is stored.
 template <int MAXW>
 __device__ inline Scal coop_apply_reset(const State& st, const Geo& g, int64_t e, Scal s, bool keep,
                                         const Row4<MAXW>& rw, int lane,
-                                        const Tables* tab = nullptr) {
+                                        const Tables* tab = nullptr, bool taken = false) {
   if ((s.flags & F_NOROOM) && lane == 0) atomicOr(st.err_bits, F_NOROOM);
   if (lane < g.G) {
     uint64_t* gb = st.grid + e * g.gstride + (int64_t)lane * g.WPR;
@@ -655,18 +674,14 @@ __device__ inline Scal coop_apply_reset(const State& st, const Geo& g, int64_t e
     for (int w = 0; w < MAXW; ++w)
       if (MAXW == 1 || w < g.WPR) gb[w] = rw.get(w);
   }
-  if (!keep) {  // reset_visits: all zero (pads 10), visit[rover] = 1 (:146-147)
+  if (!keep && !taken) {  // reset_visits: all zero (pads 10), visit[rover] = 1 (:146-147)
+    coop_fresh_visits(st, g, e, s, lane, tab);
+  } else if (keep) {  // the previous episode's rows carried into the new slot, explored map restarted
     if (lane < g.G) {
-      uint32_t* vb = st.vis + e * g.vstride + (int64_t)lane * g.NW;
-      const int bit = 4 * (s.y + 2);
-      const bool rover = lane == s.x && !(s.flags & F_NOROOM);
-      for (int w = 0; w < g.NW; ++w) {
-        uint32_t v = (tab ? tab : st.tab)->vis_pad[w];
-        if (rover && w == (bit >> 5)) v = (v & ~(0xFu << (bit & 31))) | (1u << (bit & 31));
-        vb[w] = v;
-      }
+      const uint32_t* src = vis_env(st, g, e, s.episode - 1u) + (int64_t)lane * g.NW;
+      uint32_t* dst = vis_env(st, g, e, s.episode) + (int64_t)lane * g.NW;
+      for (int w = 0; w < g.NW; ++w) dst[w] = src[w];
     }
-  } else {  // explored map restarted at the rover, bitmap mode (new_episode_visits)
     const int rc = s.x * g.G + s.y;
     for (int w = lane; w < g.estride; w += 64)
       st.expl[e * g.estride + w] = (!(s.flags & F_NOROOM) && w == (rc >> 5)) ? (1u << (rc & 31)) : 0u;

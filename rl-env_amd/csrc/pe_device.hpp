@@ -8,10 +8,15 @@
 //                                  cells on both sides: a LIDAR probe never needs a
 //                                  column bounds test (off-map == obstacle,
 //                                  plantos_env.py:271-274)
-//   vis    u32    [N][G][NW]       4-bit saturating visit counts min(v,15), padded by
+//   vis    u32    [N][2][G][NW]    4-bit saturating visit counts min(v,15), padded by
 //                                  2 cells of value 10 on both sides (off-map reads
 //                                  1.0 = min(10,10)/10, plantos_env.py:307-311).
 //                                  The nibble IS the visit count while it is < 15.
+//                                  Two slots per env: episode k's visits live in slot
+//                                  k & 1 (vis_env), so the next episode's fresh rows
+//                                  can be written ahead of time into the idle slot (the
+//                                  prefetch kernel) and an auto-reset that takes a
+//                                  prefetched record stores no visit row at all.
 //   vx     u32    [N][G*G]         exact visit count, valid only where the nibble is 15
 //                                  (plantos_env.py:203): written once at the 15th
 //                                  visit, then bumped by no-return atomics (never read
@@ -53,6 +58,7 @@ struct Geo {
   int G, C, R, D, DS;   // D = 5C+27 obs floats, DS = LDS row stride (odd)
   int WPR, NW, EW, GG;
   int64_t gstride, vstride, hstride, estride;  // per-env strides in elements
+  int64_t vslot;                               // one visit slot (G * NW words); vstride = 2 vslot
 };
 
 // Host-built constant tables (one copy per handle, global memory, read-only).
@@ -281,31 +287,38 @@ __device__ __forceinline__ void grid_set(const State& st, const Geo& g, int64_t 
   *p = w;
 }
 
+// The visit rows of env e in episode `ep` (its packed scalars' episode counter): slot ep & 1.
+__device__ __forceinline__ uint32_t* vis_env(const State& st, const Geo& g, int64_t e, uint32_t ep) {
+  return st.vis + e * g.vstride + (int64_t)(ep & 1u) * g.vslot;
+}
+
 // 5 nibbles (padded columns y..y+4 == real columns y-2..y+2) of one visit row.
-__device__ __forceinline__ uint32_t vis_window(const State& st, const Geo& g, int64_t e, int row, int y) {
+__device__ __forceinline__ uint32_t vis_window(const State& st, const Geo& g, int64_t e, uint32_t ep, int row, int y) {
   int bit = 4 * y;
-  const uint32_t* p = st.vis + e * g.vstride + (int64_t)row * g.NW + (bit >> 5);
+  const uint32_t* p = vis_env(st, g, e, ep) + (int64_t)row * g.NW + (bit >> 5);
   uint64_t two = (uint64_t)p[0] | ((uint64_t)p[1] << 32);
   return (uint32_t)(two >> (bit & 31)) & 0xFFFFFu;
 }
 
-__device__ __forceinline__ void vis_set(const State& st, const Geo& g, int64_t e, int row, int col, uint32_t v) {
+__device__ __forceinline__ void vis_set(const State& st, const Geo& g, int64_t e, uint32_t ep, int row, int col,
+                                        uint32_t v) {
   int bit = 4 * (col + 2);
-  uint32_t* p = st.vis + e * g.vstride + (int64_t)row * g.NW + (bit >> 5);
+  uint32_t* p = vis_env(st, g, e, ep) + (int64_t)row * g.NW + (bit >> 5);
   uint32_t w = *p;
   w &= ~(0xFu << (bit & 31));
   w |= v << (bit & 31);
   *p = w;
 }
 
-__device__ __forceinline__ uint32_t nibble_get(const State& st, const Geo& g, int64_t e, int row, int col) {
+__device__ __forceinline__ uint32_t nibble_get(const State& st, const Geo& g, int64_t e, uint32_t ep, int row,
+                                               int col) {
   int bit = 4 * (col + 2);
-  return (st.vis[e * g.vstride + (int64_t)row * g.NW + (bit >> 5)] >> (bit & 31)) & 15u;
+  return (vis_env(st, g, e, ep)[(int64_t)row * g.NW + (bit >> 5)] >> (bit & 31)) & 15u;
 }
 
 // exact visit count of a real cell (nibble below 15, else the u16 overflow slot)
-__device__ __forceinline__ int visit_exact(const State& st, const Geo& g, int64_t e, int row, int col) {
-  const uint32_t n = nibble_get(st, g, e, row, col);
+__device__ __forceinline__ int visit_exact(const State& st, const Geo& g, int64_t e, uint32_t ep, int row, int col) {
+  const uint32_t n = nibble_get(st, g, e, ep, row, col);
   return n < 15u ? (int)n : (int)st.vx[e * g.hstride + row * g.G + col];
 }
 
@@ -572,21 +585,31 @@ __device__ __forceinline__ Scal gen_map(const Geo& g, const Rules& rl, const Tab
 // (plantos_env.py:146-147; explored[rover] = 2 follows from it, :236).  The
 // overflow slots and the explored bitmap are not cleared: every nibble is now 0
 // (vx is read only behind a nibble of 15) and a fresh episode is in derived mode.
+// (s: the NEW episode's scalars: the rows go to its slot)
 __device__ inline void reset_visits(const State& st, const Geo& g, const Tables* tab, int64_t e, const Scal& s) {
+  uint32_t* vb = vis_env(st, g, e, s.episode);
   for (int row = 0; row < g.G; ++row)
-    for (int w = 0; w < g.NW; ++w) st.vis[e * g.vstride + (int64_t)row * g.NW + w] = tab->vis_pad[w];
-  if (!(s.flags & F_NOROOM)) vis_set(st, g, e, s.x, s.y, 1u);
+    for (int w = 0; w < g.NW; ++w) vb[(int64_t)row * g.NW + w] = tab->vis_pad[w];
+  if (!(s.flags & F_NOROOM)) vis_set(st, g, e, s.episode, s.x, s.y, 1u);
+}
+
+// The previous episode's visit rows (slot of episode - 1) into the new episode's slot.
+__device__ inline void carry_visits(const State& st, const Geo& g, int64_t e, uint32_t new_ep) {
+  const uint32_t* src = vis_env(st, g, e, new_ep - 1u);
+  uint32_t* dst = vis_env(st, g, e, new_ep);
+  for (int64_t k = 0; k < g.vslot; ++k) dst[k] = src[k];
 }
 
 // Visits of a new episode: fresh (reset_visits), or -- CurriculumWrapper carrying
-// the previous episode's counts -- left in place with only the explored map
-// restarted at the rover ({rover}, bitmap mode: explored no longer follows visits).
+// the previous episode's counts -- carried into the new slot with only the explored
+// map restarted at the rover ({rover}, bitmap mode: explored no longer follows visits).
 __device__ inline void new_episode_visits(const State& st, const Geo& g, const Tables* tab, int64_t e, Scal& s,
                                           bool keep) {
   if (!keep) {
     reset_visits(st, g, tab, e, s);
     return;
   }
+  carry_visits(st, g, e, s.episode);
   uint32_t* eb = st.expl + e * g.estride;
   for (int w = 0; w < g.estride; ++w) eb[w] = 0u;
   if (!(s.flags & F_NOROOM)) {

@@ -32,7 +32,7 @@ struct Window {
   uint32_t vlo[7], vhi[7];              // raw visit words, rows x-3 .. x+3
   int yb, ybv;                          // grid / visit column bases
 
-  __device__ __forceinline__ void load(const State& st, const Geo& g, int64_t e, int x, int y) {
+  __device__ __forceinline__ void load(const State& st, const Geo& g, int64_t e, uint32_t ep, int x, int y) {
     const uint64_t* gb = st.grid + e * g.gstride;
     yb = ONEWORD ? 0 : (y > 0 ? y - 1 : 0);
     const int w0 = (2 * yb) >> 6, o = (2 * yb) & 63;
@@ -59,7 +59,7 @@ struct Window {
     }
     ybv = y > 0 ? y - 1 : 0;
     const int vw = (4 * ybv) >> 5;
-    const uint32_t* vb = st.vis + e * g.vstride + vw;
+    const uint32_t* vb = vis_env(st, g, e, ep) + vw;
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
       const int xr = x - 3 + k;

@@ -491,7 +491,7 @@ __global__ void pe_mcts_clone_kernel(MctsArgs a) {
   const int row = c / g.G, col = c - row * g.G;
   const Scal s = unpack(a.st.scal[e]);
   const uint32_t code = (uint32_t)grid_code(a.st, g, e, row, col + g.R);
-  const uint32_t v = (uint32_t)visit_exact(a.st, g, e, row, col);
+  const uint32_t v = (uint32_t)visit_exact(a.st, g, e, s.episode, row, col);
   bool ex;
   if (s.flags & F_EXPL_BITMAP)
     ex = (a.st.expl[e * g.estride + (c >> 5)] >> (c & 31)) & 1u;

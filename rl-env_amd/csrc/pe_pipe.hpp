@@ -110,7 +110,7 @@ __device__ __forceinline__ void pipe_r2(const StepArgs& a, int64_t bb, int le, i
   const int64_t el = bb * kQuadEnvs + le;
   const int64_t elc = el < a.n ? el : (int64_t)a.n - 1;
   const int lx = (int)(r.lw.x & 0xFF);
-  const uint32_t* lvb = a.st.vis + elc * a.g.vstride;
+  const uint32_t* lvb = vis_env(a.st, a.g, elc, r.lw.w);  // (the loader env's episode: its visit slot)
 #pragma unroll
   for (int j = 0; j < JV; ++j) {
     const int xr = lx - 3 + sub + LT * j;

@@ -59,7 +59,7 @@ struct StepArgs {
 // _get_lidar_obs, plantos_env.py:251-315, into one LDS row.
 
 // Generic: runtime (G, C, R), LIDAR offsets from the handle's table.
-__device__ __forceinline__ void build_obs_generic(const StepArgs& a, int64_t e, int x, int y, float* row,
+__device__ __forceinline__ void build_obs_generic(const StepArgs& a, int64_t e, uint32_t ep, int x, int y, float* row,
                                                   const float* tdist, const float* tpos, const float* tvis,
                                                   const signed char* ldx, const signed char* ldy) {
   const Geo& g = a.g;
@@ -86,7 +86,7 @@ __device__ __forceinline__ void build_obs_generic(const StepArgs& a, int64_t e, 
   row[5 * C + 1] = tpos[y];
   for (int lx = 0; lx < 5; ++lx) {
     int xr = x + lx - 2;
-    uint32_t win = (xr >= 0 && xr < g.G) ? vis_window(a.st, g, e, xr, y) : 0xAAAAAu;
+    uint32_t win = (xr >= 0 && xr < g.G) ? vis_window(a.st, g, e, ep, xr, y) : 0xAAAAAu;
     for (int ly = 0; ly < 5; ++ly) row[5 * C + 2 + 5 * lx + ly] = tvis[(win >> (4 * ly)) & 15u];
   }
 }
@@ -181,9 +181,9 @@ __device__ __forceinline__ double transition(const StepArgs& a, int64_t e, Scal&
       if (ok) ok = grid_code(a.st, g, e, nx, ny + g.R) != OBST;
       if (ok) {
         const int cell = nx * g.G + ny;
-        const uint32_t n = nibble_get(a.st, g, e, nx, ny);
+        const uint32_t n = nibble_get(a.st, g, e, s.episode, nx, ny);
         const bool never = n == 0u;                             // :197
-        vis_set(a.st, g, e, nx, ny, n < 15u ? n + 1u : 15u);    // :203
+        vis_set(a.st, g, e, s.episode, nx, ny, n < 15u ? n + 1u : 15u);    // :203
         visit_bump_exact(a.st, g, e, cell, n);
         if (s.flags & F_EXPL_BITMAP) {
           if (expl_test_set(a.st, g, e, s.x * g.G + s.y)) s.expl++;  // explored[old] = 1, :198
@@ -429,7 +429,7 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
     const bool inb = mv && nx >= 0 && nx < g.G && ny >= 0 && ny < g.G;
     // ---- round 2: position-indexed loads
     Window<R, ONEWORD> w;
-    w.load(st, g, e, s.x, s.y);
+    w.load(st, g, e, s.episode, s.x, s.y);
     const int cell_o = s.x * g.G + s.y, cell_n = nx * g.G + ny;
     uint32_t* ep_o = st.expl + e * g.estride + (cell_o >> 5);
     uint32_t* ep_n = st.expl + e * g.estride + ((inb ? cell_n : cell_o) >> 5);
@@ -451,7 +451,7 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
         const uint32_t nib = n < 15u ? n + 1u : 15u;               // :203
         visit_bump_exact(st, g, e, cell_n, n);
         const int pb = 4 * (ny + 2) - 32 * ((4 * w.ybv) >> 5);
-        uint32_t* vrow = st.vis + e * g.vstride + (int64_t)nx * g.NW + ((4 * w.ybv) >> 5);
+        uint32_t* vrow = vis_env(st, g, e, s.episode) + (int64_t)nx * g.NW + ((4 * w.ybv) >> 5);
 #pragma unroll
         for (int k = 2; k <= 4; ++k) {
           if (k == 3 + dxm) {
@@ -717,7 +717,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         Scal ns;
         asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
         if (take(el, sv.episode, *early, rw, ns, orow)) {
-          ns = coop_apply_reset<MAXW>(st, g, el, ns, false, rw, lane, ltab);
+          ns = coop_apply_reset<MAXW>(st, g, el, ns, false, rw, lane, ltab, true);
         } else {  // the record is not this reset's (not generated yet): generate in place
           uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
           ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, false, rw, lane, scr, ltab);
@@ -775,7 +775,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         const bool took = stage ? pf_stage_take<MAXW>(stage, g, (int)a.pf.ostride, sv.episode, rw, ns, orow, lane)
                                 : (a.pf.scal && take(el, sv.episode, pl, rw, ns, orow));
         if (took) {
-          ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane, ltab);
+          ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane, ltab, true);
         } else {
           uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
           ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane, scr, ltab);
@@ -862,7 +862,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         Scal ns;
         asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
         if (a.pf.scal && take(el, sv.episode, eh ? *early : pl, rw, ns, orow)) {
-          ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane, ltab);
+          ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane, ltab, true);
         } else {
           uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
           ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane, scr, ltab);
@@ -1137,7 +1137,7 @@ __device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* 
           // nibbles): one byte store, no read of the word from memory
           const int p = m.ny + 2, b = p >> 1;
           const uint32_t wnew = (lvis[(3 + m.dxm) * LS + lane] & ~(0xFu << (4 * (p - m.ybv)))) | (nib << (4 * (p - m.ybv)));
-          st_wt(reinterpret_cast<uint8_t*>(st.vis + e * g.vstride + (int64_t)m.nx * g.NW) + b,
+          st_wt(reinterpret_cast<uint8_t*>(vis_env(st, g, e, s.episode) + (int64_t)m.nx * g.NW) + b,
                 (uint8_t)(wnew >> (4 * (2 * b - m.ybv))));
           visit_bump_exact(st, g, e, m.cell_n, n);
           if (s.flags & F_EXPL_BITMAP) {
@@ -1362,7 +1362,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
           qg[j] = *reinterpret_cast<const uint4*>(lgb + rc);
         }
       }
-      const uint32_t* lvb = st.vis + el * g.vstride;
+      const uint32_t* lvb = vis_env(st, g, el, lw.w);  // (lw.w: the loader env's episode)
       {
 #pragma unroll
         for (int j = 0; j < JV; ++j) {
@@ -1454,7 +1454,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
       }
       const int lybv = ly > 0 ? ly - 1 : 0;
       const int vw = (4 * lybv) >> 5, vo = (4 * lybv) & 31;
-      const uint32_t* vb = st.vis + el * g.vstride + vw;
+      const uint32_t* vb = vis_env(st, g, el, lw.w) + vw;
 #pragma unroll
       for (int j = 0; j < JV; ++j) {
         const int xr = lx - 3 + sub + LT * j;
@@ -1686,7 +1686,7 @@ __device__ __attribute__((noinline)) void wave_done(const StepArgs& a, int64_t e
     Scal ns;
     asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
     if (a.pf.scal && coop_take_prefetched<MAXW, KD>(a.pf, g, e, s.episode, pl, rw, ns, row, lane)) {
-      ns = coop_apply_reset<MAXW>(st, g, e, ns, keep, rw, lane);
+      ns = coop_apply_reset<MAXW>(st, g, e, ns, keep, rw, lane, nullptr, true);
     } else {
       ns = coop_reset_env<MAXW>(st, g, rl, e, s.episode, keep, rw, lane, win);
       coop_fresh_obs<MAXW>(g, rw, ns, row, tdist, tpos, tvis, st.ldx, st.ldy, lane);
@@ -1780,7 +1780,7 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
   const uint4* gsrc = reinterpret_cast<const uint4*>(st.grid + e * g.gstride + w0);
   const int vlo = s.x - 3 > 0 ? s.x - 3 : 0, vhi = s.x + 3 < G - 1 ? s.x + 3 : G - 1;
   const int nv = (vhi - vlo + 1) * NW;
-  const uint32_t* vsrc = st.vis + e * g.vstride + (int64_t)vlo * NW;
+  const uint32_t* vsrc = vis_env(st, g, e, s.episode) + (int64_t)vlo * NW;
   uint32_t eo = 0u, en = 0u;
   const int cell_o = s.x * G + s.y, cell_n = nx * G + (inb ? ny : s.y);
   if (inb && (s.flags & F_EXPL_BITMAP)) {
@@ -1929,7 +1929,7 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
     if (commit_rows) {
       if (ok) {
         const int b = (ny + 2) >> 1;  // the byte of the target's nibble in row nx
-        st_wt(reinterpret_cast<uint8_t*>(st.vis + e * g.vstride + (int64_t)nx * NW) + b,
+        st_wt(reinterpret_cast<uint8_t*>(vis_env(st, g, e, s.episode) + (int64_t)nx * NW) + b,
               (uint8_t)(wvn >> (8 * (b & 3))));
         visit_bump_exact(st, g, e, cell_n, n);
         if (s.flags & F_EXPL_BITMAP) {
@@ -2104,7 +2104,7 @@ __global__ __launch_bounds__(256) void pe_reset_coop_kernel(StepArgs a) {
     }
     if (a.obs) coop_fresh_obs<MAXW>(g, rw, ns, a.obs + e * g.D, tdist, tpos, tvis, a.st.ldx, a.st.ldy, lane);
   } else if (a.obs && lane == 0) {
-    build_obs_generic(a, e, s.x, s.y, a.obs + e * g.D, tdist, tpos, tvis, a.st.ldx, a.st.ldy);
+    build_obs_generic(a, e, s.episode, s.x, s.y, a.obs + e * g.D, tdist, tpos, tvis, a.st.ldx, a.st.ldy);
   }
 }
 
@@ -2156,6 +2156,9 @@ __global__ __launch_bounds__(256) void pe_prefetch_kernel(StepArgs a, int all) {
       for (int w = 0; w < MAXW; ++w)
         if (MAXW == 1 || w < g.WPR) dst[w] = rw.get(w);
     }
+    // the new episode's fresh visit rows into its slot -- the env's idle one (episode
+    // ep + 1 vs the running ep): the step that takes this record stores no visit row
+    coop_fresh_visits(a.st, g, e, s, lane, reinterpret_cast<const Tables*>(smem));
     if constexpr (BT)
       coop_fresh_obs<MAXW>(g, rw, s, reinterpret_cast<uint8_t*>(pf_obs_row(pf, e)), smem, smem + 72, smem + 328,
                            a.st.ldx, a.st.ldy, lane);
@@ -2210,7 +2213,7 @@ __global__ __launch_bounds__(kBlock) void pe_reset_kernel(StepArgs a) {
     if (a.obs && resetting && !scratch_ok)
       build_obs_fresh(a, a.st.grid + e * g.gstride, s, row, tdist, tpos, tvis, lldx, lldy);
     else if (a.obs && !resetting)
-      build_obs_generic(a, e, s.x, s.y, row, tdist, tpos, tvis, lldx, lldy);
+      build_obs_generic(a, e, s.episode, s.x, s.y, row, tdist, tpos, tvis, lldx, lldy);
   }
   if (!a.obs) return;
   __syncthreads();
@@ -2287,15 +2290,15 @@ __global__ void pe_get_cells_kernel(StepArgs a, uint8_t* cells, int32_t* visits,
   const int c = (int)(t - e * g.GG);
   const int row = c / g.G, col = c - row * g.G;
   if (cells) cells[t] = (uint8_t)grid_code(a.st, g, e, row, col + g.R);
-  if (visits) visits[t] = visit_exact(a.st, g, e, row, col);
+  const Scal s = unpack(a.st.scal[e]);
+  if (visits) visits[t] = visit_exact(a.st, g, e, s.episode, row, col);
   if (explored) {
-    Scal s = unpack(a.st.scal[e]);
     int8_t v;
     if (s.flags & F_EXPL_BITMAP) {
       uint32_t w = a.st.expl[e * g.estride + (c >> 5)];
       v = (w >> (c & 31)) & 1u ? 1 : 0;
     } else {
-      v = nibble_get(a.st, g, e, row, col) ? 1 : 0;  // explored_map > 0 <=> visit > 0
+      v = nibble_get(a.st, g, e, s.episode, row, col) ? 1 : 0;  // explored_map > 0 <=> visit > 0
     }
     if (v && s.x == row && s.y == col) v = 2;  // plantos_env.py:200, 236
     explored[t] = v;
@@ -2327,11 +2330,14 @@ __global__ void pe_set_env_kernel(StepArgs a, const uint8_t* cells, const int32_
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= a.n) return;
   Scal s = unpack(a.st.scal[e]);
+  // the visit rows live in the slot of the episode counter (pe_device.hpp vis_env): the
+  // new counter's, when the scalars are set too
+  const uint32_t ep0 = s.episode, ep1 = scal ? (uint32_t)scal[e * PE_NSCAL + PE_S_EPISODE] : ep0;
   uint32_t* eb = a.st.expl + e * g.estride;
   if (!(s.flags & F_EXPL_BITMAP) && visits && !explored) {
     for (int w = 0; w < g.estride; ++w) eb[w] = 0u;
     for (int c = 0; c < g.GG; ++c)
-      if (nibble_get(a.st, g, e, c / g.G, c % g.G)) eb[c >> 5] |= 1u << (c & 31);
+      if (nibble_get(a.st, g, e, ep0, c / g.G, c % g.G)) eb[c >> 5] |= 1u << (c & 31);
     s.flags |= F_EXPL_BITMAP;
   }
   if (cells) {
@@ -2344,15 +2350,18 @@ __global__ void pe_set_env_kernel(StepArgs a, const uint8_t* cells, const int32_
     }
   }
   if (visits) {
+    uint32_t* vb = vis_env(a.st, g, e, ep1);
     for (int row = 0; row < g.G; ++row) {
-      for (int w = 0; w < g.NW; ++w) a.st.vis[e * g.vstride + (int64_t)row * g.NW + w] = a.st.tab->vis_pad[w];
+      for (int w = 0; w < g.NW; ++w) vb[(int64_t)row * g.NW + w] = a.st.tab->vis_pad[w];
       for (int col = 0; col < g.G; ++col) {
         int32_t v = visits[e * g.GG + row * g.G + col];
         uint32_t vc = v <= 0 ? 0u : (uint32_t)v;
         a.st.vx[e * g.hstride + row * g.G + col] = vc;
-        vis_set(a.st, g, e, row, col, vc < 15u ? vc : 15u);
+        vis_set(a.st, g, e, ep1, row, col, vc < 15u ? vc : 15u);
       }
     }
+  } else if ((ep0 ^ ep1) & 1u) {
+    carry_visits(a.st, g, e, ep1);  // the counts move with the counter's parity
   }
   if (explored) {
     for (int w = 0; w < g.estride; ++w) {
@@ -2381,11 +2390,11 @@ __global__ void pe_set_env_kernel(StepArgs a, const uint8_t* cells, const int32_
     for (int c = 0; c < g.GG; ++c) {
       const bool bit = (eb[c >> 5] >> (c & 31)) & 1u;
       ex += bit;
-      same = same && (bit == (nibble_get(a.st, g, e, c / g.G, c % g.G) != 0u));
+      same = same && (bit == (nibble_get(a.st, g, e, ep1, c / g.G, c % g.G) != 0u));
     }
     if (same) s.flags &= ~F_EXPL_BITMAP;
   } else {
-    for (int c = 0; c < g.GG; ++c) ex += nibble_get(a.st, g, e, c / g.G, c % g.G) != 0u;
+    for (int c = 0; c < g.GG; ++c) ex += nibble_get(a.st, g, e, ep1, c / g.G, c % g.G) != 0u;
   }
   for (int row = 0; row < g.G; ++row)
     for (int w = 0; w < g.WPR; ++w) {
@@ -2395,6 +2404,21 @@ __global__ void pe_set_env_kernel(StepArgs a, const uint8_t* cells, const int32_
   s.expl = ex;
   s.total = g.GG - ob;
   a.st.scal[e] = pack(s);
+}
+
+// pe_seed(reset_episode_counters): episode := 0, an odd episode's visit rows copied
+// to slot 0 (the record of episode 1, if any, was generated into slot 1: unaffected).
+__global__ void pe_zero_episodes_kernel(StepArgs a) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.n) return;
+  uint4 w = a.st.scal[e];
+  if (w.w & 1u) {
+    const uint32_t* src = vis_env(a.st, a.g, e, 1u);
+    uint32_t* dst = vis_env(a.st, a.g, e, 0u);
+    for (int64_t k = 0; k < a.g.vslot; ++k) dst[k] = src[k];
+  }
+  w.w = 0u;
+  a.st.scal[e] = w;
 }
 
 // CurriculumWrapper.__init__ state of every env (A2C_training.py:41-54).
@@ -2820,7 +2844,9 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   if (g.NW < 4) g.NW = 4;  // 16-B visit rows: one dwordx4 per row in the sector kernel
   g.EW = (g.GG + 31) / 32;
   g.gstride = (int64_t)align_up((size_t)G * g.WPR, 2);  // 16-B aligned env blocks (row-pair loads)
-  g.vstride = (int64_t)G * g.NW;
+  // two visit slots per env, 16-B aligned (episode k's visits in slot k & 1: pe_device.hpp vis_env)
+  g.vslot = (int64_t)align_up((size_t)G * g.NW, 4);
+  g.vstride = 2 * g.vslot;
   g.hstride = (int64_t)align_up((size_t)g.GG, 8);
   // explored words; also the picks scratch of a curriculum reset that keeps visits
   g.estride = (int64_t)align_up((size_t)std::max(g.EW, (P + 1) / 2), 4);
@@ -3218,8 +3244,11 @@ int pe_seed(pe_handle* h, uint64_t seed, int32_t reset_episode_counters, void* s
   h->rl.seed = seed;
   h->cfg.seed = seed;
   if (reset_episode_counters) {
-    // the episode counter is the 4th word of each packed scalar record
-    PE_HIP(hipMemset2DAsync(reinterpret_cast<char*>(h->st.scal) + 12, sizeof(uint4), 0, 4, (size_t)h->n, s));
+    // the episode counters to 0, the visit rows of envs at an odd episode moved along
+    // (they live in the counter's slot, pe_device.hpp vis_env)
+    StepArgs a = base_args(h);
+    hipLaunchKernelGGL(pe_zero_episodes_kernel, dim3((unsigned)((h->n + 255) / 256)), dim3(256), 0, s, a);
+    PE_HIP(hipGetLastError());
   }
   return PE_OK;
 }
