@@ -79,7 +79,9 @@ typedef struct pe_config {
     int32_t num_plants;         /* P                                            */
     int32_t num_obstacles;      /* O -> O/3 clusters, plantos_env.py:341        */
     int32_t lidar_range;        /* R (device: 1..64)                            */
-    int32_t lidar_channels;     /* C (device: 1..120: [64 x D] LDS obs tile)    */
+    int32_t lidar_channels;     /* C (device: the lane-per-env kernels' [64 x D] f32 LDS
+                                   obs tile + 2CR bytes of ray offsets within 160 KiB:
+                                   C <= 120 at R <= 7, fewer rays above)         */
     int32_t max_steps;          /* 1000, plantos_env.py:120                     */
     int32_t autoreset;          /* 1: pe_step resets done envs (DummyVecEnv)    */
     double thirsty_plant_prob;  /* 0.7, plantos_env.py:26                       */

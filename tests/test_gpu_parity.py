@@ -342,6 +342,10 @@ def test_lds_bounds_of_the_ray_count():
                      device="cuda:0")
     PlantOSBatch(8, grid_size=20, num_plants=10, num_obstacles=12, lidar_range=6, lidar_channels=120,
                  device="cuda:0").close()
+    # the bound depends on R too: the ray offsets (2CR bytes) share the 160 KiB
+    with pytest.raises(ValueError, match="LDS"):
+        PlantOSBatch(8, grid_size=20, num_plants=10, num_obstacles=12, lidar_range=8, lidar_channels=120,
+                     device="cuda:0")
 
 
 def test_no_room_raises():
