@@ -16,41 +16,6 @@
 // issued after it), not vmcnt(0).
 #pragma once
 
-// Cache-policy operand of the buffer-store builtin: bit 4 = sc1 on gfx950 (write-through,
-// the line dropped from the XCD's L2 -- the obs stream must not evict the envs' state).
-constexpr int kBufSc1 = 16;
-constexpr int kBufRsrcWord3 = 0x00020000;  // raw buffer, 32-bit data format (range-checked)
-
-// Stream a full block's [64 x D] f32 obs tile (LDS) to dst: thread t0 of nt stores the
-// 16-B chunks t0, t0 + nt, ...; every chunk index past the tile is dropped by the
-// buffer's range check, so each wave issues exactly NI stores (a count the compiler's
-// wait for earlier loads relies on).
-template <int D, int NT>
-__device__ __forceinline__ void store_tile_buf(const float* rows, float* dst, int t0) {
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  constexpr int N4 = kQuadEnvs * D / 4, NI = (N4 + NT - 1) / NT;
-  static_assert((kQuadEnvs * D) % 4 == 0, "whole 16-B chunks");
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, N4 * 16, kBufRsrcWord3);
-  const v4f* sv = reinterpret_cast<const v4f*>(rows);
-  v4f v[NI];
-#pragma unroll
-  for (int j = 0; j < NI; ++j) {
-    const int k = t0 + NT * j;
-    v[j] = sv[k < N4 ? k : N4 - 1];
-  }
-#pragma unroll
-  for (int j = 0; j < NI; ++j) __builtin_amdgcn_raw_buffer_store_b128(v[j], rs, (t0 + NT * j) * 16, 0, kBufSc1);
-}
-
-// s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] |
-// vmcnt[5:4] at [15:14]) waiting on vmcnt alone
-constexpr int vmcnt_imm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14); }
-constexpr int kVmcnt0 = vmcnt_imm(0);
-// the store instructions store_tile_buf issues per wave
-template <int D, int NT>
-constexpr int tile_buf_stores() { return (kQuadEnvs * D / 4 + NT - 1) / NT; }
-static_assert(vmcnt_imm(0) == 0x0F70, "s_waitcnt vmcnt(0)");
-
 // Round-1 values of one block: the lane's env (scalars, action, return) and the
 // loader env's (scalars, whole one-word grid block: gstride / 2 <= 10 16-B units,
 // JG1 per loader thread).

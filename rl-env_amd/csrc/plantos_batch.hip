@@ -378,6 +378,41 @@ __device__ __forceinline__ void store_tile_bytes(const uint8_t* codes, uint8_t* 
   for (int k = head + t0; k < total; k += nt) dst[k] = codes[k];
 }
 
+// Cache-policy operand of the buffer-store builtin: bit 4 = sc1 on gfx950 (write-through,
+// the line dropped from the XCD's L2 -- the obs stream must not evict the envs' state).
+constexpr int kBufSc1 = 16;
+constexpr int kBufRsrcWord3 = 0x00020000;  // raw buffer, 32-bit data format (range-checked)
+
+// Stream a full block's [64 x D] f32 obs tile (LDS) to dst: thread t0 of nt stores the
+// 16-B chunks t0, t0 + nt, ...; every chunk index past the tile is dropped by the
+// buffer's range check, so each wave issues exactly NI stores (a count the compiler's
+// wait for earlier loads relies on).
+template <int D, int NT>
+__device__ __forceinline__ void store_tile_buf(const float* rows, float* dst, int t0) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  constexpr int N4 = kQuadEnvs * D / 4, NI = (N4 + NT - 1) / NT;
+  static_assert((kQuadEnvs * D) % 4 == 0, "whole 16-B chunks");
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, N4 * 16, kBufRsrcWord3);
+  const v4f* sv = reinterpret_cast<const v4f*>(rows);
+  v4f v[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int k = t0 + NT * j;
+    v[j] = sv[k < N4 ? k : N4 - 1];
+  }
+#pragma unroll
+  for (int j = 0; j < NI; ++j) __builtin_amdgcn_raw_buffer_store_b128(v[j], rs, (t0 + NT * j) * 16, 0, kBufSc1);
+}
+
+// s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] |
+// vmcnt[5:4] at [15:14]) waiting on vmcnt alone
+constexpr int vmcnt_imm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14); }
+constexpr int kVmcnt0 = vmcnt_imm(0);
+// the store instructions store_tile_buf issues per wave
+template <int D, int NT>
+constexpr int tile_buf_stores() { return (kQuadEnvs * D / 4 + NT - 1) / NT; }
+static_assert(vmcnt_imm(0) == 0x0F70, "s_waitcnt vmcnt(0)");
+
 // ------------------------------------------------------------------ kernels
 // Specialized fused step (compile-time C, R): two load rounds per lane, the rest
 // from registers (pe_fast.hpp).  Same semantics as pe_step_wave.
@@ -559,6 +594,9 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
 // lane): 64x64/C64/R32 93.8 -> 90.4 us, 40x40/C48/R8 76.7 -> 75.0, but 8x8/C16/R20
 // 68.0 -> 70.2 (sc1 16-B stores: 90.8 / 76.7 / 70.4; profiles/r3x/)
 #define PE_WAVE_ROWSTORE_MIN 200
+#endif
+#ifndef PE_QUAD_TILE_BUF
+#define PE_QUAD_TILE_BUF 0  // sector kernel's f32 tile: asm sc1 stores (0); A/B: buffer stores (1, 2)
 #endif
 #ifndef PE_STAGGER_GROUPS
 #define PE_STAGGER_GROUPS 4  // sector kernel: the grid's start-delay groups (A/B: -DPE_STAGGER_GROUPS=n)
@@ -1579,6 +1617,22 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
     } else
       store_tile(rows, a.obs + e0 * g.D, (int)valid, g.D, g.D);
   } else {
+#if PE_QUAD_TILE_BUF
+    // A/B (debug builds): the f32 tile as compiler-counted buffer stores (pe_pipe.hpp's
+    // form), by the non-commit waves (1) or by every wave (2)
+    constexpr int kTB = PE_QUAD_TILE_BUF;
+    if constexpr (!BT && !RT && EPB == kQuadEnvs) {
+      float* dst = a.obs + e0 * g.D;
+      if (valid == LS && (reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+        if (kTB == 2)
+          store_tile_buf<5 * C + 27, 64 * NW>(rows, dst, (int)threadIdx.x);
+        else if (wv != CW)
+          store_tile_buf<5 * C + 27, 64 * (NW - 1)>(rows, dst, (int)threadIdx.x);
+      } else if (wv != CW) {
+        store_tile(rows, dst, (int)valid, g.D, g.D, (int)threadIdx.x, 64 * (NW - 1));
+      }
+    } else
+#endif
     if (wv != CW) {
       if constexpr (BT) {
         if (a.obs_codes)
