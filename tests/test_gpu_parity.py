@@ -217,7 +217,9 @@ def test_rollout_parity_device_rng(name, n, steps):
                                            ("g64", True, 65536), ("g64r32", True, 65536), ("g25", False, 65536),
                                            ("g25", True, 65536),
                                            # BASELINE config 2 (16-env workgroups) and a 32-env-workgroup batch
-                                           ("g20", False, 4096), ("g20", True, 4096), ("g20", True, 20000)])
+                                           ("g20", False, 4096), ("g20", True, 4096), ("g20", True, 20000),
+                                           # the persistent pipelined kernel with a ragged last block
+                                           ("g20", True, 40001)])
 def test_full_batch_sampled_parity_and_invariants(name, desync, n):
     """65536 envs (BASELINE headline 20x20/16 rays, the 64x64/64-ray stress config,
     and 25x25/16 rays -- the geometry the reference's training scripts build,
