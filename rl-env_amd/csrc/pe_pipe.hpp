@@ -28,10 +28,12 @@ struct PipeR1 {
 };
 
 // The auto-reset path of a block with a done env, out of line: inlined into the loop
-// its registers (map generation, the cooperative reset) would be the loop's.
-__device__ __attribute__((noinline)) uint4 pipe_done(int tile_off, int lane, int wv, int64_t e0, bool done, uint4 sp,
-                                                     double ret, int ndone, bool wfix) {
-  return quad_done_path<4, true, 2, false>(kernargs(), tile_off, 16, 6, lane, wv, 3, e0, done, sp, ret, ndone, wfix);
+// its registers (map generation, the cooperative reset) would be the loop's.  `ka`:
+// the kernel's argument segment, taken by the KERNEL (kernargs()) -- in a called
+// function the kernarg-segment-pointer builtin reads as 0 on gfx950 / ROCm 7.2.
+__device__ __attribute__((noinline)) uint4 pipe_done(const void* ka, int tile_off, int lane, int wv, int64_t e0,
+                                                     bool done, uint4 sp, double ret, int ndone, bool wfix) {
+  return quad_done_path<4, true, 2, false>(ka, tile_off, 16, 6, lane, wv, 3, e0, done, sp, ret, ndone, wfix);
 }
 
 // The kernel argument re-read per iteration through an opaque copy of the kernarg
@@ -203,7 +205,8 @@ __global__ __launch_bounds__(256, WPC) void pe_step_pipe(StepArgs a0) {
                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(dmask >> 32)) << 32);
     const bool any_done = dmu != 0ull;
     const int ndone = __popcll(dmu);
-    if (__builtin_expect(any_done, 0)) s = unpack(pipe_done(tile_off, lane, wv, e0, done, pack(s), ret, ndone, wfix));
+    if (__builtin_expect(any_done, 0))
+      s = unpack(pipe_done(kernargs(), tile_off, lane, wv, e0, done, pack(s), ret, ndone, wfix));
     // ---- block bn's round 2 (its addresses need round 1), then block b's tile stores
     __builtin_amdgcn_s_waitcnt(kVmcnt0);  // block bn's round 1 landed (issued before the compute phase)
     uint4 qv[JV];
