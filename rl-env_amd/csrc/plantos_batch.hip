@@ -2428,6 +2428,10 @@ __global__ void pe_set_env_kernel(StepArgs a, const uint8_t* cells, const int32_
     }
     s.flags |= F_EXPL_BITMAP;
   }
+  // the prefetched record stays valid only if the counter stays (its key, ep0 + 1, is
+  // still the next episode's, and its fresh rows in slot (ep0 + 1) & 1 untouched): a
+  // counter moved back would turn an old key into a future one over rows since reused
+  if (a.pf.scal && ep1 != ep0) a.pf.scal[e].w = 0u;
   if (scal) {
     const int32_t* i = scal + e * PE_NSCAL;
     s.x = i[PE_S_X];
@@ -2461,7 +2465,11 @@ __global__ void pe_set_env_kernel(StepArgs a, const uint8_t* cells, const int32_
 }
 
 // pe_seed(reset_episode_counters): episode := 0, an odd episode's visit rows copied
-// to slot 0 (the record of episode 1, if any, was generated into slot 1: unaffected).
+// to slot 0.  A prefetched record keyed k promises fresh rows of episode k in slot
+// k & 1; with the counter moved back, an old key becomes a future one (an env at
+// episode 1 holds the record of episode 2, whose slot-0 rows the copy just
+// overwrote, and the counter reaches 1 again), so every record is dropped except
+// episode 1's of an env still at episode 0 (slot 1 untouched since the prefetch).
 __global__ void pe_zero_episodes_kernel(StepArgs a) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= a.n) return;
@@ -2471,6 +2479,7 @@ __global__ void pe_zero_episodes_kernel(StepArgs a) {
     uint32_t* dst = vis_env(a.st, a.g, e, 0u);
     for (int64_t k = 0; k < a.g.vslot; ++k) dst[k] = src[k];
   }
+  if (a.pf.scal && w.w != 0u) a.pf.scal[e].w = 0u;
   w.w = 0u;
   a.st.scal[e] = w;
 }

@@ -83,3 +83,22 @@ def test_set_state_episode_parity_moves_visits():
     ov.b.scal[:, O.S_EPISODE] = sc[:, O.S_EPISODE]
     _run_more(b, ov, act, seed, 90, 120)
     b.close()
+
+
+def test_set_state_counter_moved_back_drops_records():
+    """episode counters set back by one or two: an env's prefetched record of a later
+    episode would become a future key over visit rows since reused -- it must be
+    dropped (the reset then generates in place), not taken"""
+    seed, n = 47, 700
+    b, ov, act = _desync_batch(n, seed, 130)
+    st0 = b.get_state()
+    sc = np_(st0["scalars"]).copy()
+    ep = sc[:, O.S_EPISODE]
+    assert (ep >= 2).any()
+    sc[:, O.S_EPISODE] = np.maximum(ep - 1 - np.arange(n) % 2, 0)
+    b.set_state(scalars=sc)
+    st1 = b.get_state()
+    assert np.array_equal(np_(st1["visits"]), np_(st0["visits"]))
+    ov.b.scal[:, O.S_EPISODE] = sc[:, O.S_EPISODE]
+    _run_more(b, ov, act, seed, 130, 140)
+    b.close()
