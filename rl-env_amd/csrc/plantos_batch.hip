@@ -2620,8 +2620,12 @@ size_t lds_bytes(const Geo& g) {
 // (same-box A/B, profiles/r3b_ab_epb*.jsonl: 4096 envs 5.06 -> 4.55 us with 16-env
 // workgroups, 8192: 16 ~ 32, 16384: 32 best, 32768: 32 ~ 64)
 constexpr int kSmallBatch16 = 8192, kSmallBatch32 = 32768, kSmallBatch8W = 4096;
-// workgroups per CU of the persistent pipelined kernel (pe_pipe.hpp) above kSmallBatch32
-constexpr int kPipeWpc = 2;
+// workgroups per CU of the persistent pipelined kernel (pe_pipe.hpp) above kSmallBatch32;
+// 0: off.  Measured slower than pe_step_quad at every residency (same box, 65536 envs,
+// profiles/r4b/ab_pipe.jsonl: quad 9.63 us, pipe P2 12.14, P3 11.71, P4 11.54;
+// desynchronized 13.0 vs 23.5-25.4): at 2-3 workgroups per CU the compute phase runs at
+// 2-3 waves per SIMD, and P4 spills (128 VGPRs + 47 spilled).  PE_PIPE=N in debug builds.
+constexpr int kPipeWpc = 0;
 
 enum Variant {
   V_GENERIC = 0, V_C16R6_1W = 1, V_C16R6 = 2, V_C64R6 = 3,

@@ -86,9 +86,10 @@ def lib():
     L.pe_seed.argtypes = [P, U64, I32, P]
     L.pe_reset.argtypes = [P, P, P, P]
     L.pe_step.argtypes = [P, P, I32, P, P, P, P, P, P, P, P, P]
-    L.pe_step_codes.argtypes = [P, P, I32, P, P, P, P, P, P, P, P, P]
-    L.pe_obs_code_table.argtypes = [P, P]
-    L.pe_expand_obs_codes.argtypes = [P, I32, I32, P, ctypes.c_int64, P, P, P, P, P]
+    if hasattr(L, "pe_step_codes"):  # (ABI 4; an older library loaded for a same-box A/B lacks them)
+        L.pe_step_codes.argtypes = [P, P, I32, P, P, P, P, P, P, P, P, P]
+        L.pe_obs_code_table.argtypes = [P, P]
+        L.pe_expand_obs_codes.argtypes = [P, I32, I32, P, ctypes.c_int64, P, P, P, P, P]
     L.pe_get_info.argtypes = [P, P, P]
     L.pe_get_state.argtypes = [P, P, P, P, P, P]
     L.pe_set_state.argtypes = [P, P, P, P, P, P]
@@ -128,7 +129,8 @@ def lib():
                  "pe_curriculum_get", "pe_mcts_create", "pe_mcts_destroy", "pe_mcts_seed", "pe_mcts_set_rng",
                  "pe_mcts_get_rng", "pe_mcts_search", "pe_step_codes", "pe_obs_code_table",
                  "pe_expand_obs_codes"):
-        getattr(L, name).restype = ctypes.c_int
+        if hasattr(L, name):
+            getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
 
