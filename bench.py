@@ -68,8 +68,10 @@ def parse():
                         "pipelined; the line's 'gather' object; 0: skip it)")
     p.add_argument("--graph", type=int, default=64,
                    help="capture up to this many consecutive steps in one hipGraph and replay it (0: one host "
-                        "launch per step); every captured step is a full pe_step launch; a window of K <= this "
-                        "many steps is ONE K-step graph")
+                        "launch per step); every captured step is a full pe_step launch")
+    p.add_argument("--short-window", choices=("graph", "direct"), default="graph",
+                   help="a window of <= 256 steps: one captured graph of its steps (graph), or one host launch "
+                        "per step (direct)")
     p.add_argument("--desync", action="store_true",
                    help="time the desynchronized episode mix as the headline window (default: synchronized "
                         "fresh episodes, desync as the secondary 'desync' object)")
@@ -201,20 +203,24 @@ def upload_graph(torch, gr):
         return False
 
 
-DIRECT_MAX = 256  # windows of at most this many steps: direct launches (see plan_graph)
+DIRECT_MAX = 256  # windows of at most this many steps: the short-window plan (see plan_graph)
 
 
-def plan_graph(K, graph_max, pf):
+def plan_graph(K, graph_max, pf, short="graph"):
     """Steps per captured graph for a K-step window (0: direct launches).  A short
-    window (K <= DIRECT_MAX, e.g. the driver's 20 steps) is direct launches: the first
-    replay of a freshly captured graph ran ~0.4-2 us per step slower than later ones,
-    and slower than direct launches, whose host cost hides behind the kernels
-    (--steps 20: 10.26-10.35 us per step direct vs 10.5-12.4 graph, alternating runs,
-    profiles/r3p_drv_ab.jsonl).  A longer one replays a graph whose length is a
-    multiple of the prefetch cadence pf (every replay then holds the same share of
-    prefetch launches), the rest as direct launches."""
-    if graph_max <= 1 or K <= DIRECT_MAX:
+    window (K <= DIRECT_MAX, e.g. the driver's 20 steps) is ONE K-step graph, captured
+    and uploaded before the warm-up (direct launches): host launches cost 7-14 us per
+    pe_step in the first tens of calls after a synchronize (profiles/r4j_host_cost.json),
+    above the ~9.6 us kernel, so a direct-launch window times the host (same box,
+    alternating runs, profiles/r4l_drv_ab.jsonl: direct 12.8-14.3 us per step, one graph
+    11.6-13.2, 5-step graphs warmed by the warm-up 11.8-13.1).  short="direct": direct
+    launches.  A longer window replays a graph whose length is a multiple of the
+    prefetch cadence pf (every replay then holds the same share of prefetch launches),
+    the rest as direct launches."""
+    if graph_max <= 1:
         return 0
+    if K <= DIRECT_MAX:
+        return K if short == "graph" else 0
     if K <= graph_max:
         return K
     chunk = graph_max
@@ -508,7 +514,7 @@ def main():
     # right up to the timed window: a GPU left idle while the host captures starts the
     # window below its clocks (driver-shaped 20-step windows: ~1 us per step)
     pf = b.prefetch_every
-    chunk = plan_graph(K, args.graph, pf)
+    chunk = plan_graph(K, args.graph, pf, args.short_window)
     graph = capture(chunk)
     for t in range(args.warmup):
         one_step(t)

@@ -36,12 +36,13 @@ def test_launcher_starts_n_ranks_gloo():
 
 
 def test_graph_plan_and_launch_label():
-    """the driver's short window (--steps 20) is direct launches, long windows replay
+    """the driver's short window (--steps 20) is one captured graph, long windows replay
     graphs aligned to the prefetch cadence, and the line's launch label says what the
     timed loop executed"""
     sys.path.insert(0, REPO)
     import bench
-    assert bench.plan_graph(20, 64, 256) == 0
+    assert bench.plan_graph(20, 64, 256) == 20  # the driver's window: one 20-step graph
+    assert bench.plan_graph(20, 64, 256, "direct") == 0
     assert bench.launch_label(20, 0) == "20 direct host launches (one pe_step per step)"
     assert bench.plan_graph(153000, 64, 256) == 256
     assert bench.launch_label(1000, 256) == "hipGraph: 3 replays of 256 captured pe_step launches + 232 direct host launches"

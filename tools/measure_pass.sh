@@ -1,0 +1,27 @@
+#!/usr/bin/env bash
+# The measurement pass of the product library (tools/gpu_session.sh steps): the GPU suite,
+# smoke, bench lines of every geometry, rocprof kernel stats and FETCH / WRITE PMC passes.
+# Copy it into profiles/ with tools/summarize_pass.sh TAG.
+#   usage: bash tools/measure_pass.sh TAG
+set -euo pipefail
+OUT=gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
+T=$1
+bash tools/gpu_session.sh $T tests
+tail -n 1 $OUT/tests_$T.log
+bash tools/gpu_session.sh $T smoke bench benchx:drv:--steps_20_--warmup_5 bench64 \
+  benchx:n4096:--envs_4096_--steps_20000_--warmup_1000_--desync-steps_20000_--cpu-seconds_5 \
+  benchx:g25:--grid_25_--steps_20000_--warmup_1000_--cpu-seconds_5 \
+  benchx:g21:--grid_21_--rays_10_--range_2_--plants_8_--obstacles_50_--steps_20000_--warmup_1000_--cpu-seconds_5 \
+  benchx:g15:--grid_15_--rays_16_--range_4_--plants_6_--obstacles_8_--steps_20000_--warmup_1000_--cpu-seconds_5 \
+  benchx:g32:--grid_32_--rays_24_--range_9_--plants_20_--obstacles_30_--steps_4000_--warmup_200_--desync-steps_4000_--cpu-seconds_5 \
+  benchx:g64r32:--grid_64_--rays_64_--range_32_--steps_2000_--warmup_100_--desync-steps_2000_--cpu-seconds_5 \
+  benchx:g40c48:--grid_40_--rays_48_--range_8_--steps_2000_--warmup_100_--desync-steps_2000_--cpu-seconds_5 \
+  stats statsd stats64 \
+  statsx:n4096:--envs_4096_--steps_4096_--warmup_200_--desync-steps_0_--gather-steps_0_--no-cpu-baseline \
+  statsx:g25:--grid_25_--steps_4096_--warmup_200_--desync-steps_0_--gather-steps_0_--no-cpu-baseline \
+  statsx:g64r32:--grid_64_--rays_64_--range_32_--steps_1000_--warmup_50_--desync-steps_0_--gather-steps_0_--no-cpu-baseline \
+  statsx:g40c48:--grid_40_--rays_48_--range_8_--steps_1000_--warmup_50_--desync-steps_0_--gather-steps_0_--no-cpu-baseline \
+  pmcf pmcw pmcf64 pmcw64 pmcx:g25:FETCH_SIZE:--grid_25 pmcx:g25:WRITE_SIZE:--grid_25 \
+  pmcx:n4096:FETCH_SIZE:--envs_4096 pmcx:n4096:WRITE_SIZE:--envs_4096 \
+  pmcx:g64r32:FETCH_SIZE:--grid_64_--rays_64_--range_32 pmcx:g64r32:WRITE_SIZE:--grid_64_--rays_64_--range_32
+echo pass done

@@ -4,7 +4,7 @@
 bench number -- read the SHARES and the timeline shape, not the length).
 
   python tools/stamps.py build                 # CPU: build/stamps/libplantos_hip_stamps.so
-  python tools/stamps.py run [--grid 20 --rays 16 --envs 65536]   # GPU
+  python tools/stamps.py run [--grid 20 --rays 16 --envs 65536] [--lib build/ab/lib_X.so]   # GPU
 
 Stamps (lane 0 of each wave, 100 MHz = 10 ns ticks):
   0 entry  1 round-1 data in  2 round-2 loads landed + LDS written  3 after barrier
@@ -38,6 +38,8 @@ def pct(v, q):
 def run(argv):
     abl = int(argv[argv.index("--ablate") + 1]) if "--ablate" in argv else 0
     os.environ["PLANTOS_HIP_LIB"] = SO if not abl else SO.replace(".so", f"_abl{abl}.so")
+    if "--lib" in argv:  # a stamped A/B library (tools/ab_build.sh with EXTRA_FLAGS=-DPE_STAMPS)
+        os.environ["PLANTOS_HIP_LIB"] = argv[argv.index("--lib") + 1]
     sys.path.insert(0, os.path.join(REPO, "rl-env_amd"))
     import numpy as np
     import torch
