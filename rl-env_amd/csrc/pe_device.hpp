@@ -20,7 +20,14 @@
 //   vx     u32    [N][G*G]         exact visit count, valid only where the nibble is 15
 //                                  (plantos_env.py:203): written once at the 15th
 //                                  visit, then bumped by no-return atomics (never read
-//                                  by the step kernels); never cleared
+//                                  by the step kernels); never cleared.  A step defers
+//                                  its write (vpend): scattered writes to cold lines
+//                                  issued at the commit held the end of the launch
+//   vpend  u32    [N]              the overflow write of an env's last step (vx_pending:
+//                                  cell | SET15 / INC, 0 = none), applied by the commit
+//                                  lane of the next step at the start of its compute
+//                                  phase, or by pe_vx_flush_kernel before any API call
+//                                  that reads or replaces the counts
 //   expl   u32    [N][EW]          explored bitmap (explored_map > 0), authoritative
 //                                  only in F_EXPL_BITMAP mode; otherwise explored is
 //                                  derived: explored_map > 0  <=>  visit > 0 (true for
@@ -91,6 +98,7 @@ struct State {
   uint64_t* grid;
   uint32_t* vis;
   uint32_t* vx;    // visit-count overflow slots (see layout above)
+  uint32_t* vpend; // each env's deferred overflow write (see layout above)
   uint32_t* expl;
   const Tables* tab;
   const signed char* ldx;  // [C][R] LIDAR offsets (generic kernel)
@@ -322,15 +330,31 @@ __device__ __forceinline__ int visit_exact(const State& st, const Geo& g, int64_
   return n < 15u ? (int)n : (int)st.vx[e * g.hstride + row * g.G + col];
 }
 
-// visit_counts[cell] += 1 (plantos_env.py:203) given the cell's current nibble n:
-// the overflow slot is set at the 15th visit and bumped in memory after that.
+// visit_counts[cell] += 1 (plantos_env.py:203) given the cell's current nibble n: the
+// overflow slot is set at the 15th visit and bumped in memory after that.  The sector
+// and lane kernels defer that write as a vpend entry (vx_pending), store it, and apply
+// the previous step's early in the next launch (vx_apply; the same lane, program
+// order): a write to vx issued at the commit -- one per ~100 env-steps, each to a cold
+// line of a 105 MB array at 65536 envs -- held the launch's end (profiles/r4p/,
+// r4q/).  The one-wave-per-env kernel writes at once (visit_bump_exact): its handles
+// never hold a pending word.
+enum : uint32_t { VP_SET15 = 1u << 31, VP_INC = 1u << 30, VP_CELL = VP_INC - 1u };
+__device__ __forceinline__ uint32_t vx_pending(int cell, uint32_t n) {
+  return n == 14u ? (VP_SET15 | (uint32_t)cell) : (n == 15u ? (VP_INC | (uint32_t)cell) : 0u);
+}
 __device__ __forceinline__ void visit_bump_exact(const State& st, const Geo& g, int64_t e, int cell, uint32_t n) {
   uint32_t* vp = st.vx + e * g.hstride + cell;
-  if (n == 14u) {
+  if (n == 14u)
     *vp = 15u;
-  } else if (n == 15u) {
+  else if (n == 15u)
     atomicAdd(vp, 1u);  // no-return atomic: the count is never read by a step
-  }
+}
+__device__ __forceinline__ void vx_apply(const State& st, const Geo& g, int64_t e, uint32_t p) {
+  uint32_t* vp = st.vx + e * g.hstride + (p & VP_CELL);
+  if (p & VP_SET15)
+    *vp = 15u;
+  else
+    atomicAdd(vp, 1u);  // no-return atomic: the count is never read by a step
 }
 
 __device__ __forceinline__ bool expl_test_set(const State& st, const Geo& g, int64_t e, int cell) {

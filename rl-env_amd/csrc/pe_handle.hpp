@@ -38,3 +38,6 @@ struct pe_handle {
 
 // pe_internal_set_error (plantos_batch.hip): records pe_last_error() for this thread.
 extern "C" int pe_internal_set_error(int code, const char* msg);
+// pe_internal_flush_vx (plantos_batch.hip): the steps' deferred visit-overflow writes applied
+// on `stream` (before anything reads the exact visit counts, e.g. the MCTS clone).
+extern "C" int pe_internal_flush_vx(const pe_handle* h, void* stream);

@@ -1101,6 +1101,8 @@ int pe_mcts_search(pe_mcts* m, const uint8_t* mask, int32_t* actions, int32_t* r
     a.ldsp = ldsp;
   }
   if (cells > 0) {
+    // the steps' deferred visit-overflow writes first: the clone reads the exact counts
+    if (const int fr = pe_internal_flush_vx(h, s)) return fr;
     hipLaunchKernelGGL(pe_mcts_clone_kernel, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, a);
     if (use_lds)
       hipLaunchKernelGGL(pe_mcts_search_lds_kernel, dim3((unsigned)((h->n + 63) / 64)), dim3(64), lds, s, a);

@@ -25,6 +25,7 @@ struct PipeR1 {
   uint4 sw, lw, q[JG1];
   int32_t alo, ahi;
   double ret;
+  uint32_t vp;  // the commit wave's: the deferred overflow write (pe_device.hpp vx_pending)
 };
 
 // The auto-reset path of a block with a done env, out of line: inlined into the loop
@@ -61,6 +62,7 @@ __device__ __forceinline__ void pipe_r1(const StepArgs& a, int64_t bb, int lane,
   r.alo = ap[ec << ash];
   r.ahi = ap[(ec << ash) + ash];
   r.ret = st.ep_ret[cw ? ec : 0];  // (the commit wave's; the others read one shared word)
+  r.vp = st.vpend[cw ? ec : 0];
   r.lw = st.scal[elc];
   const uint4* lgq = reinterpret_cast<const uint4*>(st.grid + elc * a.g.gstride);
 #pragma unroll
@@ -192,7 +194,7 @@ __global__ __launch_bounds__(256, WPC) void pe_step_pipe(StepArgs a0) {
     if (wv == CW) __builtin_amdgcn_s_setprio(2);  // the commit wave is the laggard (pe_step_quad)
     bool done = false, wfix = false;
     quad_compute<C, R, true, NW, false, false, true>(a, lrow, lvis, rows, tdist, tpos, tvis, lane, wv, e, live, C, R,
-                                                     m, 0u, 0u, 0.0, s, ret, done, wfix);
+                                                     m, 0u, 0u, 0.0, cur.vp, s, ret, done, wfix);
     if (wv == CW) {
       const uint64_t dm = __ballot(done);
       if (lane == 0) reinterpret_cast<uint64_t*>(smem)[35] = dm;

@@ -136,28 +136,44 @@ __device__ __forceinline__ void quad_rays(const uint64_t* lrow, int lane, int kc
 }
 
 // Runtime-(C, R) sector rays: the ray march of pe_step_quad<0, 0, ...> (the table-
-// driven sector kernel of geometries with no compile-time specialization, C <= 32,
+// driven sector kernel of geometries with no compile-time specialization, C <= 64,
 // 2 <= R <= 14).  Wave wv's rays [wv*C/NW, (wv+1)*C/NW); the probe offsets are
 // wave-uniform (the packed (dx & 0xFF | dy << 8) table st.ldxy, R rounded up to 8
-// per ray: scalar loads), so a probe is one LDS read of the window row at the lane's
-// row offset, a shift and the same 2-bit packing as quad_rays (first hit by one
+// per ray and zero-padded): 8 probes per 16-B scalar load, unrolled, so that a ray's
+// LDS reads are in flight together instead of one scalar-load round trip and one LDS
+// round trip per probe; a probe is one LDS read of the window row at the lane's row
+// offset, a shift and the same 2-bit packing as quad_rays (first hit by one
 // find-first-set; plantos_env.py:260-292).
 template <typename OT>
 __device__ __forceinline__ void quad_rays_rt(const uint64_t* lrow, const int16_t* ldxy, int i0, int i1, int R,
                                              int lane, int kc, int sh, bool watered, OT* row, const float* tdist) {
   const int RP = (R + 7) & ~7;
-  const uint32_t kNZ = 0x55555555u & ((1u << (2 * R)) - 1u);
+  const uint32_t kNZ = 0x55555555u & ((1u << (2 * R)) - 1u);  // R <= 14
   const float4* tone = reinterpret_cast<const float4*>(tdist + kOneHotF);
   const uint64_t wclr = ~((uint64_t)(watered ? 1u : 0u) << (sh + 2 * R));  // the rover's cell: 3 -> 2 (watered)
   for (int i = i0; i < i1; ++i) {
-    const int16_t* o = ldxy + i * RP;
+    const uint4* o4 = reinterpret_cast<const uint4*>(ldxy + i * RP);  // (16-B aligned: RP is a multiple of 8)
     uint32_t pk = 0u;
-    for (int r = 0; r < R; ++r) {
-      const int v = o[r];
-      const int dx = (int)(int8_t)(v & 0xFF), dy = (int)(int8_t)((v >> 8) & 0xFF);
+    auto probe = [&](uint32_t v, int r) {
+      const int dx = (int)(int8_t)(v & 0xFFu), dy = (int)(int8_t)((v >> 8) & 0xFFu);
       uint64_t w = lrow[(kc + dx) * kQuadEnvs + lane];
-      if (dx == 0) w &= wclr;  // (uniform)
-      pk |= (uint32_t)((w >> (sh + 2 * (dy + R))) & 3u) << (2 * r);
+      w &= dx == 0 ? wclr : ~0ull;
+      pk |= (uint32_t)((w >> (sh + 2 * (dy + R))) & 3u) << (2 * r);  // (r < R <= 14)
+    };
+    int r0 = 0;
+    for (; r0 + 8 <= R; r0 += 8) {  // whole chunks: 8 probes unrolled, their LDS reads in flight together
+      const uint4 q = o4[r0 >> 3];
+      const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) probe(qw[j >> 1] >> (16 * (j & 1)), r0 + j);
+    }
+    if (r0 < R) {  // the last R % 8 probes: one scalar load, then a loop (padded probes not marched:
+                   // R = 9 marching all 16 was 10 % slower than the per-probe loads, profiles/r4m)
+      const uint4 q = o4[r0 >> 3];
+      for (int j = 0; j < R - r0; ++j) {
+        const uint32_t qj = j < 2 ? q.x : (j < 4 ? q.y : (j < 6 ? q.z : q.w));
+        probe(qj >> (16 * (j & 1)), r0 + j);
+      }
     }
     const uint32_t nz = ((pk | (pk >> 1)) & kNZ) | (1u << (2 * R));
     const int f = __builtin_ctz(nz);        // 2r of the first hit, 2R if none

@@ -159,71 +159,6 @@ __device__ inline void build_obs_fresh_codes(const StepArgs& a, const uint64_t* 
     }
 }
 
-// ------------------------------------------------------------------ transition
-// PlantOSEnv.step without the observation (plantos_env.py:160-183, 185-222).
-__device__ __forceinline__ double transition(const StepArgs& a, int64_t e, Scal& s, int64_t action, bool& term,
-                                             bool& trunc) {
-  const Geo& g = a.g;
-  const Rules& rl = a.rl;
-  s.step = s.step < 65535 ? s.step + 1 : 65535;  // :162
-  double h = 0.0;
-  if (action < 4) {                                // :166
-    int64_t ai = action < 0 ? action + 4 : action; // Python negative list index
-    if (ai < 0) {
-      s.flags |= F_POISON_ACT;                     // reference: IndexError
-      atomicOr(a.st.err_bits, F_POISON_ACT);
-    } else {
-      // directions (:186) N,E,S,W = (-1,0),(0,1),(1,0),(0,-1)
-      const int dxm = ai == 0 ? -1 : (ai == 2 ? 1 : 0);
-      const int dym = ai == 1 ? 1 : (ai == 3 ? -1 : 0);
-      const int nx = s.x + dxm, ny = s.y + dym;
-      bool ok = nx >= 0 && nx < g.G && ny >= 0 && ny < g.G;  // :193-195
-      if (ok) ok = grid_code(a.st, g, e, nx, ny + g.R) != OBST;
-      if (ok) {
-        const int cell = nx * g.G + ny;
-        const uint32_t n = nibble_get(a.st, g, e, s.episode, nx, ny);
-        const bool never = n == 0u;                             // :197
-        vis_set(a.st, g, e, s.episode, nx, ny, n < 15u ? n + 1u : 15u);    // :203
-        visit_bump_exact(a.st, g, e, cell, n);
-        if (s.flags & F_EXPL_BITMAP) {
-          if (expl_test_set(a.st, g, e, s.x * g.G + s.y)) s.expl++;  // explored[old] = 1, :198
-          if (expl_test_set(a.st, g, e, cell)) s.expl++;             // explored[new] = 2, :200
-        } else if (never) {
-          s.expl++;  // derived mode: explored[old] is set, explored[new] was 0 iff never visited
-        }
-        s.x = nx;                                                  // :199
-        s.y = ny;
-        h = never ? rl.r_exploration : rl.r_revisit;               // :204-207
-      } else {
-        s.flags |= F_COLLIDED;                                     // :209
-        s.coll = s.coll < 65535 ? s.coll + 1 : 65535;              // :210
-        h = rl.r_invalid;                                          // :211
-      }
-    }
-  } else {
-    const int code = grid_code(a.st, g, e, s.x, s.y + g.R);
-    if (code == THIRSTY) {                                         // fork plantos_env_new.py:237-240
-      grid_set(a.st, g, e, s.x, s.y + g.R, HYD);
-      h = rl.r_goal;
-    } else if (code == HYD) {                                      // fork :241-242 (root raises)
-      h = rl.r_mistake;
-      if (!(s.flags & F_POISON_HYD)) atomicOr(a.st.err_bits, F_POISON_HYD);
-      s.flags |= F_POISON_HYD;
-    } else {
-      h = rl.r_water_empty;                                        // :221-222
-    }
-  }
-  double rew = rl.r_step;                                          // :164
-  rew += h;
-  // exploration_percentage >= 100  <=>  explored >= total  (:176, 244-246, 331)
-  term = s.expl >= s.total;
-  trunc = s.step >= rl.max_steps;                                  // :177
-  if (term && !(s.flags & F_BONUS)) {                              // :179-181
-    rew += rl.r_complete;
-    s.flags |= F_BONUS;
-  }
-  return rew;
-}
 
 __device__ __forceinline__ void load_tables(float* smem, const Tables* tab) {
   const float* src = reinterpret_cast<const float*>(tab);
@@ -433,11 +368,13 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
   uint4 sw = make_uint4(0u, 0u, 0u, 0u);
   int64_t action = 0;
   double ret = 0.0;
+  uint32_t vp0 = 0u;  // the previous step's deferred overflow write (pe_device.hpp vx_pending)
   if (live) {
     sw = st.scal[e];
     action = a.act_bytes == 8 ? reinterpret_cast<const int64_t*>(a.actions)[e]
                               : (int64_t)reinterpret_cast<const int32_t*>(a.actions)[e];
     ret = st.ep_ret[e];
+    vp0 = st.vpend[e];
   }
   load_tables(smem, st.tab);
   const Tables* ltab = reinterpret_cast<const Tables*>(smem);
@@ -465,6 +402,8 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
     // ---- round 2: position-indexed loads
     Window<R, ONEWORD> w;
     w.load(st, g, e, s.episode, s.x, s.y);
+    if (vp0) vx_apply(st, g, e, vp0);
+    uint32_t np = 0u;
     const int cell_o = s.x * g.G + s.y, cell_n = nx * g.G + ny;
     uint32_t* ep_o = st.expl + e * g.estride + (cell_o >> 5);
     uint32_t* ep_n = st.expl + e * g.estride + ((inb ? cell_n : cell_o) >> 5);
@@ -484,7 +423,7 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
         const uint32_t n = (sel3<uint32_t>(dxm, w.vis32(2), w.vis32(3), w.vis32(4)) >> (4 * (ny + 2 - w.ybv))) & 15u;
         const bool never = n == 0u;                                // :197
         const uint32_t nib = n < 15u ? n + 1u : 15u;               // :203
-        visit_bump_exact(st, g, e, cell_n, n);
+        np = vx_pending(cell_n, n);
         const int pb = 4 * (ny + 2) - 32 * ((4 * w.ybv) >> 5);
         uint32_t* vrow = vis_env(st, g, e, s.episode) + (int64_t)nx * g.NW + ((4 * w.ybv) >> 5);
 #pragma unroll
@@ -567,7 +506,12 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
       if (a.ep_len_out) a.ep_len_out[e] = s.step;
       if (a.tinfo) write_info(a.st, a.g, ltab, e, s, a.tinfo + e * PE_NINFO);
     }
+    {
+      const uint32_t npw = (term || trunc) && a.autoreset ? 0u : np;  // (a reset's new rows need none)
+      if (vp0 | npw) st.vpend[e] = npw;
+    }
     if ((term || trunc) && a.autoreset) {                          // DummyVecEnv auto-reset
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the overflow write landed: reset_env's scratch is vx
       s = reset_env(st, g, rl, ltab, e, s.episode);
       st.ep_ret[e] = 0.0;
       st.scal[e] = pack(s);
@@ -1050,8 +994,8 @@ __device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* 
                                              typename std::conditional<BT, uint8_t, float>::type* rows,
                                              const float* tdist, const float* tpos, const float* tvis, int lane,
                                              int wv, int64_t e, bool live, int Cr, int Rr, const QuadMove& m,
-                                             uint32_t eo, uint32_t en, double cthr, Scal& s, double& ret,
-                                             bool& done, bool& wfix) {
+                                             uint32_t eo, uint32_t en, double cthr, uint32_t vp0, Scal& s,
+                                             double& ret, bool& done, bool& wfix) {
   using OT = typename std::conditional<BT, uint8_t, float>::type;
   constexpr int LS = kQuadEnvs, CW = NW - 1;
   const Geo& g = a.g;
@@ -1062,6 +1006,10 @@ __device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* 
   const uint64_t* gb = st.grid + e * g.gstride;
   done = false;
   wfix = false;
+  // the previous step's deferred overflow write (pe_device.hpp vx_pending), issued now:
+  // every load the commit wave waits for before its stores has landed at the barrier
+  if (wv == CW && live && vp0) vx_apply(st, g, e, vp0);
+  uint32_t np = 0u;
   s.step = s.step < 65535 ? s.step + 1 : 65535;                  // :162
   bool ok = false, watered = false, wet_hyd = false;
   uint32_t n = 0u;
@@ -1177,7 +1125,7 @@ __device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* 
           const uint32_t wnew = (lvis[(3 + m.dxm) * LS + lane] & ~(0xFu << (4 * (p - m.ybv)))) | (nib << (4 * (p - m.ybv)));
           st_wt(reinterpret_cast<uint8_t*>(vis_env(st, g, e, s.episode) + (int64_t)m.nx * g.NW) + b,
                 (uint8_t)(wnew >> (4 * (2 * b - m.ybv))));
-          visit_bump_exact(st, g, e, m.cell_n, n);
+          np = vx_pending(m.cell_n, n);
           if (s.flags & F_EXPL_BITMAP) {
             uint32_t* ep_o = st.expl + e * g.estride + (m.cell_o >> 5);
             uint32_t* ep_n = st.expl + e * g.estride + (m.cell_n >> 5);
@@ -1212,6 +1160,7 @@ __device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* 
         st_wt(st.ep_ret + e, ret);
         st_wt(st.scal + e, pack(s));
       }
+      if (vp0 | np) st_wt(st.vpend + e, np);
     }
   }
 }
@@ -1280,6 +1229,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   const int32_t* ap = reinterpret_cast<const int32_t*>(a.actions);
   const int32_t alo = ap[ec << ash], ahi = ap[(ec << ash) + ash];
   double ret = st.ep_ret[wv == CW ? ec : 0];  // (the commit wave's; the others read one shared word)
+  const uint32_t vp0 = st.vpend[wv == CW ? ec : 0];  // (the commit wave's: the deferred overflow write)
   // (Tried: the loader env's position by a bpermute from lane le of the wave instead of
   // this load -- 64x64 24.5 -> 25.2 us, 25x25 desync +0.4 us, the headline unchanged;
   // profiles/r3m_ab_*.jsonl.)
@@ -1565,7 +1515,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // 9.47 -> 9.59; profiles/r3i_ab_*.jsonl.)
   bool done = false, wfix = false;
   quad_compute<C, R, ONEWORD, NW, BT, RT>(a, lrow, lvis, rows, tdist, tpos, tvis, lane, wv, e, live, Cr, Rr, m, eo, en,
-                                          cthr, s, ret, done, wfix);
+                                          cthr, vp0, s, ret, done, wfix);
   PE_STAMP(4);
   // ---- DummyVecEnv auto-reset (rare): commit wave, after the whole obs row is in LDS
   // any env of the block done (the usual answer: no)?  The commit wave's done mask
@@ -1658,7 +1608,9 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   PE_STAMP(7);
 }
 
+#ifdef PE_DEBUG_KNOBS  // the persistent pipelined kernel: a debug-build A/B only (measured slower)
 #include "pe_pipe.hpp"
+#endif
 
 // ---------------------------------------------------------------- pe_step_wave
 // The fused step for every geometry without a compile-time sector kernel (any
@@ -1985,6 +1937,9 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
         const int b = (ny + 2) >> 1;  // the byte of the target's nibble in row nx
         st_wt(reinterpret_cast<uint8_t*>(vis_env(st, g, e, s.episode) + (int64_t)nx * NW) + b,
               (uint8_t)(wvn >> (8 * (b & 3))));
+        // (written here, not deferred through vpend as in the sector kernels: holding the
+        // pending word across this kernel spilled 29 more SGPRs, 64x64/R32 85.8 -> 90.2 us,
+        // profiles/r4q/ab_g64r32.jsonl)
         visit_bump_exact(st, g, e, cell_n, n);
         if (s.flags & F_EXPL_BITMAP) {
           if (wo != eo) st.expl[e * g.estride + (cell_o >> 5)] = wo;
@@ -2484,6 +2439,18 @@ __global__ void pe_zero_episodes_kernel(StepArgs a) {
   a.st.scal[e] = w;
 }
 
+// The deferred overflow writes (pe_device.hpp vx_pending) of every env applied and
+// cleared: before any API call that reads the exact visit counts or replaces them.
+__global__ void pe_vx_flush_kernel(StepArgs a) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.n) return;
+  const uint32_t p = a.st.vpend[e];
+  if (p) {
+    vx_apply(a.st, a.g, e, p);
+    a.st.vpend[e] = 0u;
+  }
+}
+
 // CurriculumWrapper.__init__ state of every env (A2C_training.py:41-54).
 __global__ void pe_cur_init_kernel(CurRec* cur, int n, double thr) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2620,12 +2587,11 @@ size_t lds_bytes(const Geo& g) {
 // (same-box A/B, profiles/r3b_ab_epb*.jsonl: 4096 envs 5.06 -> 4.55 us with 16-env
 // workgroups, 8192: 16 ~ 32, 16384: 32 best, 32768: 32 ~ 64)
 constexpr int kSmallBatch16 = 8192, kSmallBatch32 = 32768, kSmallBatch8W = 4096;
-// workgroups per CU of the persistent pipelined kernel (pe_pipe.hpp) above kSmallBatch32;
-// 0: off.  Measured slower than pe_step_quad at every residency (same box, 65536 envs,
-// profiles/r4b/ab_pipe.jsonl: quad 9.63 us, pipe P2 12.14, P3 11.71, P4 11.54;
-// desynchronized 13.0 vs 23.5-25.4): at 2-3 workgroups per CU the compute phase runs at
-// 2-3 waves per SIMD, and P4 spills (128 VGPRs + 47 spilled).  PE_PIPE=N in debug builds.
-constexpr int kPipeWpc = 0;
+// The persistent pipelined kernel (pe_pipe.hpp) is compiled into debug builds only
+// (PE_PIPE=P workgroups per CU): measured slower than pe_step_quad at every residency
+// (same box, 65536 envs, profiles/r4b/ab_pipe.jsonl: quad 9.63 us, pipe P2 12.14, P3
+// 11.71, P4 11.54; desynchronized 13.0 vs 23.5-25.4): at 2-3 workgroups per CU the
+// compute phase runs at 2-3 waves per SIMD, and P4 spills (128 VGPRs + 47 spilled).
 
 enum Variant {
   V_GENERIC = 0, V_C16R6_1W = 1, V_C16R6 = 2, V_C64R6 = 3,
@@ -2649,6 +2615,7 @@ size_t quad_lds_bytes(const Geo& g, bool codes) {
 
 bool is_quad(int v) { return v >= V_QUAD_C16R6_1W; }
 
+#ifdef PE_DEBUG_KNOBS
 // the persistent pipelined kernel's grid and LDS: min(blocks, WPC per CU); the LDS
 // request caps residency at WPC workgroups per CU (the grid assumes it)
 int launch_pipe(const pe_handle* h, const StepArgs& a, hipStream_t s) {
@@ -2665,9 +2632,12 @@ int launch_pipe(const pe_handle* h, const StepArgs& a, hipStream_t s) {
   PE_HIP(hipGetLastError());
   return PE_OK;
 }
+#endif
 
 int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
+#ifdef PE_DEBUG_KNOBS
   if (h->pipe_wpc > 0) return launch_pipe(h, a, s);
+#endif
   if (is_quad(h->variant)) {
     const int nw = h->quad_waves, epb = h->quad_epb;
     dim3 grid((unsigned)((h->n + epb - 1) / epb)), block(nw * 64);
@@ -3081,12 +3051,13 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
       h->quad_epb = v == 16 || (v == 32 && h->quad_waves == 4) ? v : kQuadEnvs;  // 8 waves: 16 or 64
     }
 #endif
-  // the persistent pipelined kernel (pe_pipe.hpp): the headline geometry's 64-env,
-  // 4-wave, f32-tile kernel at batches that fill the chip
   h->num_cus = prop.multiProcessorCount;
-  h->pipe_wpc = n_envs > kSmallBatch32 ? kPipeWpc : 0;
+  h->pipe_wpc = 0;
 #ifdef PE_DEBUG_KNOBS
-  if (const char* pp = std::getenv("PE_PIPE")) h->pipe_wpc = std::min(std::max(std::atoi(pp), 0), 4);
+  // the persistent pipelined kernel (pe_pipe.hpp, A/B): the headline geometry's 64-env,
+  // 4-wave, f32-tile kernel at batches that fill the chip
+  if (const char* pp = std::getenv("PE_PIPE"))
+    h->pipe_wpc = n_envs > kSmallBatch32 ? std::min(std::max(std::atoi(pp), 0), 4) : 0;
 #endif
   if (h->pipe_wpc == 1) h->pipe_wpc = 2;
   if (!(h->variant == V_QUAD_C16R6_1W && h->quad_epb == kQuadEnvs && h->quad_waves == 4 && !h->tile_codes))
@@ -3132,6 +3103,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   const size_t o_grid = carve(n * (size_t)g.gstride * 8);
   const size_t o_vis = carve(n * (size_t)g.vstride * 4);
   const size_t o_vx = carve(n * (size_t)g.hstride * 4);
+  const size_t o_vpend = carve(n * sizeof(uint32_t));
   const size_t o_expl = carve(n * (size_t)g.estride * 4);
   h->bytes = off;
   hipError_t me = hipMalloc(&h->mem, h->bytes);
@@ -3152,6 +3124,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   h->st.grid = reinterpret_cast<uint64_t*>(base + o_grid);
   h->st.vis = reinterpret_cast<uint32_t*>(base + o_vis);
   h->st.vx = reinterpret_cast<uint32_t*>(base + o_vx);
+  h->st.vpend = reinterpret_cast<uint32_t*>(base + o_vpend);
   h->st.expl = reinterpret_cast<uint32_t*>(base + o_expl);
   int rc = PE_OK;
   if (h->pf_every > 0) {
@@ -3320,6 +3293,19 @@ int pe_seed(pe_handle* h, uint64_t seed, int32_t reset_episode_counters, void* s
   return PE_OK;
 }
 
+// The steps' deferred overflow writes applied (pe_vx_flush_kernel), before a call that
+// reads the exact visit counts (state export, the MCTS clone) or replaces them (set
+// state, resets: reset_env's map scratch is the overflow array).
+int flush_vx(const pe_handle* h, hipStream_t s) {
+  hipLaunchKernelGGL(pe_vx_flush_kernel, dim3((unsigned)((h->n + 255) / 256)), dim3(256), 0, s, base_args(h));
+  PE_HIP(hipGetLastError());
+  return PE_OK;
+}
+
+extern "C" int pe_internal_flush_vx(const pe_handle* h, void* stream) {
+  return flush_vx(h, static_cast<hipStream_t>(stream));
+}
+
 int pe_reset(pe_handle* h, const uint8_t* mask, float* obs, void* stream) {
   if (!h) return fail(PE_ERR_ARG, "null handle");
   DeviceGuard dg(h);
@@ -3327,6 +3313,7 @@ int pe_reset(pe_handle* h, const uint8_t* mask, float* obs, void* stream) {
   StepArgs a = base_args(h);
   a.mask = mask;
   a.obs = obs;
+  if (const int fr = flush_vx(h, static_cast<hipStream_t>(stream))) return fr;
   const int rc = launch_reset(h, a, static_cast<hipStream_t>(stream));
   if (rc != PE_OK || h->pf_every <= 0) return rc;
   return launch_prefetch(h, static_cast<hipStream_t>(stream), 1);  // the new episodes' next maps
@@ -3430,6 +3417,8 @@ int pe_get_state(pe_handle* h, uint8_t* cells, int32_t* visits, int8_t* explored
   if (dg.rc) return dg.rc;
   StepArgs a = base_args(h);
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (visits)
+    if (const int fr = flush_vx(h, s)) return fr;
   if (cells || visits || explored) {
     int64_t total = (int64_t)h->n * h->g.GG;
     hipLaunchKernelGGL(pe_get_cells_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a, cells, visits,
@@ -3450,6 +3439,7 @@ int pe_set_state(pe_handle* h, const uint8_t* cells, const int32_t* visits, cons
   if (dg.rc) return dg.rc;
   StepArgs a = base_args(h);
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (const int fr = flush_vx(h, s)) return fr;
   hipLaunchKernelGGL(pe_set_env_kernel, dim3((h->n + 127) / 128), dim3(128), 0, s, a, cells, visits, explored, scalars);
   PE_HIP(hipGetLastError());
   return PE_OK;
@@ -3463,6 +3453,7 @@ int pe_load_maps(pe_handle* h, int32_t k, const int32_t* env_index, const uint8_
   if (dg.rc) return dg.rc;
   StepArgs a = base_args(h);
   a.obs = obs_k;
+  if (const int fr = flush_vx(h, static_cast<hipStream_t>(stream))) return fr;
   hipLaunchKernelGGL(pe_load_maps_kernel, dim3((k + kBlock - 1) / kBlock), dim3(kBlock), lds_bytes(h->g),
                      static_cast<hipStream_t>(stream), a, k, env_index, cells, rover);
   PE_HIP(hipGetLastError());
