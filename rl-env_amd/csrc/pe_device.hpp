@@ -24,10 +24,11 @@
 //                                  its write (vpend): scattered writes to cold lines
 //                                  issued at the commit held the end of the launch
 //   vpend  u32    [N]              the overflow write of an env's last step (vx_pending:
-//                                  cell | SET15 / INC, 0 = none), applied by the commit
-//                                  lane of the next step at the start of its compute
-//                                  phase, or by pe_vx_flush_kernel before any API call
-//                                  that reads or replaces the counts
+//                                  cell | SET15 / INC, 0 = none; the headline kernel
+//                                  only), applied by the commit lane of the next step at
+//                                  the start of its compute phase, or by
+//                                  pe_vx_flush_kernel before any API call that reads or
+//                                  replaces the counts
 //   expl   u32    [N][EW]          explored bitmap (explored_map > 0), authoritative
 //                                  only in F_EXPL_BITMAP mode; otherwise explored is
 //                                  derived: explored_map > 0  <=>  visit > 0 (true for
@@ -331,13 +332,13 @@ __device__ __forceinline__ int visit_exact(const State& st, const Geo& g, int64_
 }
 
 // visit_counts[cell] += 1 (plantos_env.py:203) given the cell's current nibble n: the
-// overflow slot is set at the 15th visit and bumped in memory after that.  The sector
-// and lane kernels defer that write as a vpend entry (vx_pending), store it, and apply
-// the previous step's early in the next launch (vx_apply; the same lane, program
-// order): a write to vx issued at the commit -- one per ~100 env-steps, each to a cold
-// line of a 105 MB array at 65536 envs -- held the launch's end (profiles/r4p/,
-// r4q/).  The one-wave-per-env kernel writes at once (visit_bump_exact): its handles
-// never hold a pending word.
+// overflow slot is set at the 15th visit and bumped in memory after that.  The
+// headline sector kernel (pe_step_quad<C16,R6,1word>, 64 envs) defers that write as a
+// vpend entry (vx_pending), stores it, and applies the previous step's early in the next
+// launch (vx_apply; the same lane, program order): a write to vx issued at the commit --
+// one per ~100 env-steps, each to a cold line of a 105 MB array at 65536 envs -- held
+// the launch's end (profiles/r4p/, r4q/).  Every other step kernel writes at once
+// (visit_bump_exact): their handles never hold a pending word.
 enum : uint32_t { VP_SET15 = 1u << 31, VP_INC = 1u << 30, VP_CELL = VP_INC - 1u };
 __device__ __forceinline__ uint32_t vx_pending(int cell, uint32_t n) {
   return n == 14u ? (VP_SET15 | (uint32_t)cell) : (n == 15u ? (VP_INC | (uint32_t)cell) : 0u);

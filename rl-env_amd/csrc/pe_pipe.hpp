@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256, WPC) void pe_step_pipe(StepArgs a0) {
     double ret = cur.ret;
     if (wv == CW) __builtin_amdgcn_s_setprio(2);  // the commit wave is the laggard (pe_step_quad)
     bool done = false, wfix = false;
-    quad_compute<C, R, true, NW, false, false, true>(a, lrow, lvis, rows, tdist, tpos, tvis, lane, wv, e, live, C, R,
+    quad_compute<C, R, true, NW, false, false, true, true>(a, lrow, lvis, rows, tdist, tpos, tvis, lane, wv, e, live, C, R,
                                                      m, 0u, 0u, 0.0, cur.vp, s, ret, done, wfix);
     if (wv == CW) {
       const uint64_t dm = __ballot(done);

@@ -368,13 +368,11 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
   uint4 sw = make_uint4(0u, 0u, 0u, 0u);
   int64_t action = 0;
   double ret = 0.0;
-  uint32_t vp0 = 0u;  // the previous step's deferred overflow write (pe_device.hpp vx_pending)
   if (live) {
     sw = st.scal[e];
     action = a.act_bytes == 8 ? reinterpret_cast<const int64_t*>(a.actions)[e]
                               : (int64_t)reinterpret_cast<const int32_t*>(a.actions)[e];
     ret = st.ep_ret[e];
-    vp0 = st.vpend[e];
   }
   load_tables(smem, st.tab);
   const Tables* ltab = reinterpret_cast<const Tables*>(smem);
@@ -402,8 +400,6 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
     // ---- round 2: position-indexed loads
     Window<R, ONEWORD> w;
     w.load(st, g, e, s.episode, s.x, s.y);
-    if (vp0) vx_apply(st, g, e, vp0);
-    uint32_t np = 0u;
     const int cell_o = s.x * g.G + s.y, cell_n = nx * g.G + ny;
     uint32_t* ep_o = st.expl + e * g.estride + (cell_o >> 5);
     uint32_t* ep_n = st.expl + e * g.estride + ((inb ? cell_n : cell_o) >> 5);
@@ -423,7 +419,7 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
         const uint32_t n = (sel3<uint32_t>(dxm, w.vis32(2), w.vis32(3), w.vis32(4)) >> (4 * (ny + 2 - w.ybv))) & 15u;
         const bool never = n == 0u;                                // :197
         const uint32_t nib = n < 15u ? n + 1u : 15u;               // :203
-        np = vx_pending(cell_n, n);
+        visit_bump_exact(st, g, e, cell_n, n);
         const int pb = 4 * (ny + 2) - 32 * ((4 * w.ybv) >> 5);
         uint32_t* vrow = vis_env(st, g, e, s.episode) + (int64_t)nx * g.NW + ((4 * w.ybv) >> 5);
 #pragma unroll
@@ -506,12 +502,7 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
       if (a.ep_len_out) a.ep_len_out[e] = s.step;
       if (a.tinfo) write_info(a.st, a.g, ltab, e, s, a.tinfo + e * PE_NINFO);
     }
-    {
-      const uint32_t npw = (term || trunc) && a.autoreset ? 0u : np;  // (a reset's new rows need none)
-      if (vp0 | npw) st.vpend[e] = npw;
-    }
     if ((term || trunc) && a.autoreset) {                          // DummyVecEnv auto-reset
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the overflow write landed: reset_env's scratch is vx
       s = reset_env(st, g, rl, ltab, e, s.episode);
       st.ep_ret[e] = 0.0;
       st.scal[e] = pack(s);
@@ -989,7 +980,7 @@ __device__ __forceinline__ void quad_move_cells(QuadMove& m, const Scal& s, int 
 // threshold, loaded by the caller with round 2, or (LX) here by the commit wave in the
 // modes that need them -- the persistent kernel keeps other loads in flight here, and
 // a wait for a value loaded one iteration earlier is a vmcnt(0).
-template <int C, int R, bool ONEWORD, int NW, bool BT, bool RT, bool LX = false>
+template <int C, int R, bool ONEWORD, int NW, bool BT, bool RT, bool LX = false, bool DV = false>
 __device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* lrow, const uint32_t* lvis,
                                              typename std::conditional<BT, uint8_t, float>::type* rows,
                                              const float* tdist, const float* tpos, const float* tvis, int lane,
@@ -1006,9 +997,11 @@ __device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* 
   const uint64_t* gb = st.grid + e * g.gstride;
   done = false;
   wfix = false;
-  // the previous step's deferred overflow write (pe_device.hpp vx_pending), issued now:
-  // every load the commit wave waits for before its stores has landed at the barrier
-  if (wv == CW && live && vp0) vx_apply(st, g, e, vp0);
+  // DV: the previous step's deferred overflow write (pe_device.hpp vx_pending), issued
+  // now: every load the commit wave waits for before its stores has landed at the barrier
+  if constexpr (DV) {
+    if (wv == CW && live && vp0) vx_apply(st, g, e, vp0);
+  }
   uint32_t np = 0u;
   s.step = s.step < 65535 ? s.step + 1 : 65535;                  // :162
   bool ok = false, watered = false, wet_hyd = false;
@@ -1125,7 +1118,10 @@ __device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* 
           const uint32_t wnew = (lvis[(3 + m.dxm) * LS + lane] & ~(0xFu << (4 * (p - m.ybv)))) | (nib << (4 * (p - m.ybv)));
           st_wt(reinterpret_cast<uint8_t*>(vis_env(st, g, e, s.episode) + (int64_t)m.nx * g.NW) + b,
                 (uint8_t)(wnew >> (4 * (2 * b - m.ybv))));
-          np = vx_pending(m.cell_n, n);
+          if constexpr (DV)
+            np = vx_pending(m.cell_n, n);
+          else
+            visit_bump_exact(st, g, e, m.cell_n, n);
           if (s.flags & F_EXPL_BITMAP) {
             uint32_t* ep_o = st.expl + e * g.estride + (m.cell_o >> 5);
             uint32_t* ep_n = st.expl + e * g.estride + (m.cell_n >> 5);
@@ -1160,7 +1156,9 @@ __device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* 
         st_wt(st.ep_ret + e, ret);
         st_wt(st.scal + e, pack(s));
       }
-      if (vp0 | np) st_wt(st.vpend + e, np);
+      if constexpr (DV) {
+        if (vp0 | np) st_wt(st.vpend + e, np);
+      }
     }
   }
 }
@@ -1229,7 +1227,12 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   const int32_t* ap = reinterpret_cast<const int32_t*>(a.actions);
   const int32_t alo = ap[ec << ash], ahi = ap[(ec << ash) + ash];
   double ret = st.ep_ret[wv == CW ? ec : 0];  // (the commit wave's; the others read one shared word)
-  const uint32_t vp0 = st.vpend[wv == CW ? ec : 0];  // (the commit wave's: the deferred overflow write)
+  // the deferred overflow write (pe_device.hpp vx_pending): the headline instantiation
+  // only -- measured faster there (9.66 -> 9.52 us), slower in the constructor default's
+  // multi-word C10R2 kernel (8.22 -> 8.69) and the 16-env small-batch shape (4.44 -> 4.61),
+  // profiles/r4q/, r4v/
+  constexpr bool DV = C == 16 && R == 6 && ONEWORD && NW == 4 && !BT && EPB == kQuadEnvs;
+  const uint32_t vp0 = DV ? st.vpend[wv == CW ? ec : 0] : 0u;  // (the commit wave's)
   // (Tried: the loader env's position by a bpermute from lane le of the wave instead of
   // this load -- 64x64 24.5 -> 25.2 us, 25x25 desync +0.4 us, the headline unchanged;
   // profiles/r3m_ab_*.jsonl.)
@@ -1514,8 +1517,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // re-using their data registers -- desynchronized 11.12 -> 12.05 us, synchronized
   // 9.47 -> 9.59; profiles/r3i_ab_*.jsonl.)
   bool done = false, wfix = false;
-  quad_compute<C, R, ONEWORD, NW, BT, RT>(a, lrow, lvis, rows, tdist, tpos, tvis, lane, wv, e, live, Cr, Rr, m, eo, en,
-                                          cthr, vp0, s, ret, done, wfix);
+  quad_compute<C, R, ONEWORD, NW, BT, RT, false, DV>(a, lrow, lvis, rows, tdist, tpos, tvis, lane, wv, e, live, Cr,
+                                                     Rr, m, eo, en, cthr, vp0, s, ret, done, wfix);
   PE_STAMP(4);
   // ---- DummyVecEnv auto-reset (rare): commit wave, after the whole obs row is in LDS
   // any env of the block done (the usual answer: no)?  The commit wave's done mask
@@ -1937,7 +1940,7 @@ __global__ __launch_bounds__(64 * kWaveEnvs) __attribute__((amdgpu_waves_per_eu(
         const int b = (ny + 2) >> 1;  // the byte of the target's nibble in row nx
         st_wt(reinterpret_cast<uint8_t*>(vis_env(st, g, e, s.episode) + (int64_t)nx * NW) + b,
               (uint8_t)(wvn >> (8 * (b & 3))));
-        // (written here, not deferred through vpend as in the sector kernels: holding the
+        // (written here, not deferred through vpend as in the headline kernel: holding the
         // pending word across this kernel spilled 29 more SGPRs, 64x64/R32 85.8 -> 90.2 us,
         // profiles/r4q/ab_g64r32.jsonl)
         visit_bump_exact(st, g, e, cell_n, n);
