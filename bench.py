@@ -70,8 +70,8 @@ def parse():
                    help="capture up to this many consecutive steps in one hipGraph and replay it (0: one host "
                         "launch per step); every captured step is a full pe_step launch")
     p.add_argument("--short-window", choices=("graph", "direct"), default="graph",
-                   help="a window of <= 256 steps: one captured graph of its steps (graph), or one host launch "
-                        "per step (direct)")
+                   help="a window of <= 256 steps: one captured graph of its steps after the warm-up steps as "
+                        "one captured graph (graph), or one host launch per step (direct)")
     p.add_argument("--desync", action="store_true",
                    help="time the desynchronized episode mix as the headline window (default: synchronized "
                         "fresh episodes, desync as the secondary 'desync' object)")
@@ -212,7 +212,7 @@ DIRECT_MAX = 256  # windows of at most this many steps: the short-window plan (s
 def plan_graph(K, graph_max, pf, short="graph"):
     """Steps per captured graph for a K-step window (0: direct launches).  A short
     window (K <= DIRECT_MAX, e.g. the driver's 20 steps) is ONE K-step graph, captured
-    and uploaded before the warm-up (direct launches): host launches cost 7-14 us per
+    and uploaded before the warm-up (itself one W-step graph, see main): host launches cost 7-14 us per
     pe_step in the first tens of calls after a synchronize (profiles/r4j_host_cost.json),
     above the ~9.6 us kernel, so a direct-launch window times the host (same box,
     alternating runs, profiles/r4l_drv_ab.jsonl: direct 12.8-14.3 us per step, one graph
@@ -519,8 +519,15 @@ def main():
     pf = b.prefetch_every
     chunk = plan_graph(K, args.graph, pf, args.short_window)
     graph = capture(chunk)
-    for t in range(args.warmup):
-        one_step(t)
+    # the short window's W warm-up steps as one captured W-step graph: the first graph replay
+    # of a process pays more than later ones, so the window's is not the first
+    # (profiles/r4aa_drv_ab.jsonl: 11.2 us per step median vs 12.1 with direct warm-up steps)
+    wgraph = capture(args.warmup) if chunk and K <= DIRECT_MAX and args.warmup > 0 else None
+    if wgraph is not None:
+        wgraph.replay()
+    else:
+        for t in range(args.warmup):
+            one_step(t)
     torch.cuda.synchronize()
     ep0 = episodes(b)
     elapsed, kern_ms = timed(torch, dist, device, K, one_step, chunk, graph)
@@ -595,7 +602,8 @@ def main():
                        "envs_per_gpu": n, "grid": G, "rays": C, "lidar_range": R,
                        "parallelism": f"env-shard x{world} (independent replicas; RCCL gather leg: 'gather')",
                        "kernel": b.kernel_name,
-                       "launch": launch_label(K, chunk)},
+                       "launch": launch_label(K, chunk) + (f" (warm-up: one {args.warmup}-step graph)"
+                                                           if K <= DIRECT_MAX and chunk and args.warmup > 0 else "")},
             "resets_in_window": resets,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
