@@ -270,9 +270,15 @@ def test_full_batch_sampled_parity_and_invariants(name, desync, n):
             assert np.isin(lid[:, :, 0], dist).all(), t
             assert np.isin(ob[:, 5 * C:5 * C + 2], posv).all(), t
             assert np.isin(ob[:, 5 * C + 2:], visv).all(), t
-    st = b.get_state(parts=("scalars",))
+    st = b.get_state(parts=("scalars", "visits"))
     s = np_(st["scalars"])
     assert (s[sample] == ov.b.scal).all()
+    # exact visit counts, past 15 too: the headline kernel defers its overflow writes to the
+    # next step (pe_device.hpp vx_pending), get_state applies the pending ones first
+    vis = np_(st["visits"][torch.as_tensor(sample, device=st["visits"].device)])
+    assert (vis == ov.b.visits.reshape(vis.shape)).all()
+    if desync and G <= 25:  # episodes of up to ~1000 steps at the end: the overflow path ran
+        assert (vis >= 15).any()
     # a random policy never finishes a map: every episode ends at the truncation
     assert (s[:, O.S_EPISODE] == 1 + (start + steps) // 1000).all()
     assert (s[:, O.S_STEP] == (start + steps) % 1000).all()
