@@ -998,9 +998,12 @@ __device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* 
   done = false;
   wfix = false;
   // DV: the previous step's deferred overflow write (pe_device.hpp vx_pending), issued
-  // now: every load the commit wave waits for before its stores has landed at the barrier
+  // now by wave 0 (not the commit wave, the block's laggard; desynchronized 10.71 ->
+  // 10.60 us with the compaction below, profiles/r4ad/): every load the wave waits for
+  // has landed at the barrier.  (Ordered before a same-kernel lane-path reset of the env,
+  // which uses vx as scratch, by that path's __syncthreads.)
   if constexpr (DV) {
-    if (wv == CW && live && vp0) vx_apply(st, g, e, vp0);
+    if (wv == 0 && live && vp0) vx_apply(st, g, e, vp0);
   }
   uint32_t np = 0u;
   s.step = s.step < 65535 ? s.step + 1 : 65535;                  // :162
@@ -1232,7 +1235,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // multi-word C10R2 kernel (8.22 -> 8.69) and the 16-env small-batch shape (4.44 -> 4.61),
   // profiles/r4q/, r4v/
   constexpr bool DV = C == 16 && R == 6 && ONEWORD && NW == 4 && !BT && EPB == kQuadEnvs;
-  const uint32_t vp0 = DV ? st.vpend[wv == CW ? ec : 0] : 0u;  // (the commit wave's)
+  const uint32_t vp0 = DV ? st.vpend[wv == CW || wv == 0 ? ec : 0] : 0u;  // (wave 0 applies, CW stores)
   // (Tried: the loader env's position by a bpermute from lane le of the wave instead of
   // this load -- 64x64 24.5 -> 25.2 us, 25x25 desync +0.4 us, the headline unchanged;
   // profiles/r3m_ab_*.jsonl.)
@@ -2121,17 +2124,25 @@ __global__ __launch_bounds__(256) void pe_reset_coop_kernel(StepArgs a) {
 }
 
 // The envs flagged by step kernels since the last prefetch launch, compacted into
-// pf.queue (one wave per 64 envs, one atomic per wave with a flagged env), flags
-// cleared.  Runs right before the queue-mode prefetch launch, on the same stream.
+// pf.queue (256 envs per workgroup, one atomic per workgroup with a flagged env: one per
+// wave was 1024 atomics on one counter), flags cleared.  Runs right before the
+// queue-mode prefetch launch, on the same stream.
 __global__ __launch_bounds__(256) void pe_pf_compact_kernel(Prefetch pf, int n) {
   const int lane = threadIdx.x & 63;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const bool f = e < n && pf.flag[e] != 0;
   const uint64_t m = __ballot(f);
-  if (m == 0ull) return;  // wave-uniform
-  uint32_t base = 0u;
-  if (lane == 0) base = atomicAdd(pf.qn, (uint32_t)__popcll(m));
-  base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+  __shared__ uint32_t wc[4], bb;
+  const int w = threadIdx.x >> 6;
+  if (lane == 0) wc[w] = (uint32_t)__popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t tot = wc[0] + wc[1] + wc[2] + wc[3];
+    bb = tot ? atomicAdd(pf.qn, tot) : 0u;
+  }
+  __syncthreads();
+  uint32_t base = bb;
+  for (int k = 0; k < w; ++k) base += wc[k];
   if (f) {
     pf.queue[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)e;
     pf.flag[e] = 0;
