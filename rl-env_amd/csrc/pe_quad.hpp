@@ -139,9 +139,10 @@ __device__ __forceinline__ void quad_rays(const uint64_t* lrow, int lane, int kc
 // driven sector kernel of geometries with no compile-time specialization, C <= 64,
 // 2 <= R <= 14).  Wave wv's rays [wv*C/NW, (wv+1)*C/NW); the probe offsets are
 // wave-uniform (the packed (dx & 0xFF | dy << 8) table st.ldxy, R rounded up to 8
-// per ray and zero-padded): 8 probes per 16-B scalar load, unrolled, so that a ray's
-// LDS reads are in flight together instead of one scalar-load round trip and one LDS
-// round trip per probe; a probe is one LDS read of the window row at the lane's row
+// per ray and zero-padded, copied into LDS by the kernel: read from global memory it
+// was a vector load per 8-probe chunk that each ray waited out): 8 probes per 16-B LDS
+// read at a wave-uniform address, unrolled, so that a ray's window reads are in flight
+// together instead of one round trip per probe; a probe is one LDS read of the window row at the lane's row
 // offset, a shift and the same 2-bit packing as quad_rays (first hit by one
 // find-first-set; plantos_env.py:260-292).
 template <typename OT>
@@ -151,6 +152,9 @@ __device__ __forceinline__ void quad_rays_rt(const uint64_t* lrow, const int16_t
   const uint32_t kNZ = 0x55555555u & ((1u << (2 * R)) - 1u);  // R <= 14
   const float4* tone = reinterpret_cast<const float4*>(tdist + kOneHotF);
   const uint64_t wclr = ~((uint64_t)(watered ? 1u : 0u) << (sh + 2 * R));  // the rover's cell: 3 -> 2 (watered)
+  // (tried: the lane's row base and shift folded in once, the watered fix-up per ray
+  // instead of per probe -- 5 VALU per probe instead of ~11, measured slower: 40x40/C48/R8
+  // 31.10 -> 31.40 us, profiles/r4af/)
   for (int i = i0; i < i1; ++i) {
     const uint4* o4 = reinterpret_cast<const uint4*>(ldxy + i * RP);  // (16-B aligned: RP is a multiple of 8)
     uint32_t pk = 0u;

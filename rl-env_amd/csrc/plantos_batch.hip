@@ -601,6 +601,13 @@ constexpr int quad_ctab_off() {
 __host__ __device__ constexpr int quad_ctab_off_rt(int R, int C) {
   return quad_tile_off_rt(R) + ((kQuadEnvs * (5 * C + 27) + 15) / 16) * 4;
 }
+// offset (floats) from the tile to what follows it (+ the code table)
+__host__ __device__ constexpr int quad_rtab_off(int C, bool bt) {
+  return bt ? ((kQuadEnvs * (5 * C + 27) + 15) / 16) * 4 + 256 : kQuadEnvs * (5 * C + 27);
+}
+// the runtime sector kernel's probe table in LDS (floats; C rays x R rounded up to 8
+// int16 entries), placed after the tile (+ code table) and before the staging region
+__host__ __device__ constexpr int quad_rtab_floats(int C, int R) { return ((C * ((R + 7) & ~7) * 2 + 15) / 16) * 4; }
 
 // ---- pe_step_quad's auto-reset slow path (a block with a done env), out of line:
 // kept in separate functions so that their register demand (map generation, the
@@ -1044,7 +1051,8 @@ __device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* 
     const int sh = 2 * (yp - m.yb);
     const int vs = 4 * (yp - m.ybv);
     if constexpr (RT) {
-      quad_rays_rt<OT>(lrow, st.ldxy, wv * Cr / NW, (wv + 1) * Cr / NW, Rr, lane, kc, sh, watered, row, tdist);
+      const int16_t* ltab = reinterpret_cast<const int16_t*>(reinterpret_cast<const float*>(rows) + quad_rtab_off(Cr, BT));
+      quad_rays_rt<OT>(lrow, ltab, wv * Cr / NW, (wv + 1) * Cr / NW, Rr, lane, kc, sh, watered, row, tdist);
     } else {
       sector_rays<C, R, NW>(wv, lrow, lane, kc, sh, watered, row, tdist);
     }
@@ -1184,6 +1192,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   constexpr int NR = 2 * RM + 3, NV = 7, LS = kQuadEnvs, CW = NW - 1;  // CW: commit wave
   const int NRL = RT ? 2 * Rr + 3 : NR;  // window rows (the LDS layout's)
   const int tile_off = RT ? quad_tile_off_rt(Rr) : quad_tile_off<RM>();
+  // after the tile (+ code table): RT's probe table (quad_rtab_off), then the staging region
+  const int tail_off = tile_off + quad_rtab_off(Cr, BT);
   static_assert(EPB == 16 || EPB == 32 || EPB == 64, "envs per workgroup");
   static_assert(!BT || EPB == kQuadEnvs, "the byte-coded kernel's LDS-DMA staging predicts over all 64 lanes");
 
@@ -1263,6 +1273,12 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   if constexpr (BT) {
     if (threadIdx.x < 256) ctab[threadIdx.x] = obs_code_value(st.tab, Rr, g.G, (int)threadIdx.x);
   }
+  if constexpr (RT) {  // the probe table (st.ldxy) into LDS: read from global memory in the ray
+                       // loop, each 8-probe chunk was a vector load waited out with vmcnt(0)
+    const uint4* src = reinterpret_cast<const uint4*>(st.ldxy);
+    uint4* dst = reinterpret_cast<uint4*>(smem + tail_off);
+    for (int k = threadIdx.x; k < Cr * ((Rr + 7) & ~7) / 8; k += blockDim.x) dst[k] = src[k];
+  }
   Scal s = unpack(sw);
 #ifdef PE_STAMPS
   if ((int)(s.x + lw.x) == -12345) g_stamps[0] = 1;  // consume round 1 before the stamp
@@ -1280,8 +1296,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // only (64x64 desynchronized: 36.6 -> 36.2 us): at 20x20 the waits hipcc places
   // around a possibly outstanding LDS-DMA (a vmcnt(0) at the next use of any load
   // result) serialize round 2 in every block (9.39 -> 10.0 us, desync 11.52 -> 12.29).
-  float* stage = smem + (BT ? (RT ? quad_ctab_off_rt(Rr, Cr) : quad_ctab_off<RM, CM>()) + 256
-                            : tile_off + LS * (5 * Cr + 27));
+  float* stage = smem + tail_off + (RT ? quad_rtab_floats(Cr, Rr) : 0);
   const bool stage_ok = BT && a.pf.scal && quad_coop(a, 1) && e0 + EPB <= a.n;  // full block: every lane live
   const bool stage_info = !st.cur && a.tinfo && pf_stage_info_fits(g.G, g.WPR, (int)a.pf.ostride);
   // (issued right after round 2's own loads: hipcc drains every memory op in flight
@@ -2618,8 +2633,9 @@ enum Variant {
 // the prefetched records' obs row stride (bytes; pe_device.hpp Prefetch)
 size_t pf_ostride(const Geo& g, bool codes) { return align_up((size_t)(codes ? g.D : 4 * g.D), 16); }
 
-size_t quad_lds_bytes(const Geo& g, bool codes) {
-  const size_t off = (size_t)((kTabFloats + (2 * g.R + 3) * kQuadEnvs * 2 + 7 * kQuadEnvs + 3) & ~3);
+size_t quad_lds_bytes(const Geo& g, bool codes, bool rt) {
+  const size_t off = (size_t)((kTabFloats + (2 * g.R + 3) * kQuadEnvs * 2 + 7 * kQuadEnvs + 3) & ~3) +
+                     (rt ? (size_t)quad_rtab_floats(g.C, g.R) : 0);  // (+ the runtime kernel's probe table)
   // + the single-done record's LDS-DMA staging region (pe_coop.hpp pf_stage_issue)
   const size_t stage = (size_t)pf_stage_bytes(g.G, g.WPR, (int)pf_ostride(g, codes));
   if (codes)  // byte tile + code table (quad_ctab_off)
@@ -2636,7 +2652,7 @@ int launch_pipe(const pe_handle* h, const StepArgs& a, hipStream_t s) {
   const int wpc = h->pipe_wpc;
   const int64_t nblk = ((int64_t)h->n + kQuadEnvs - 1) / kQuadEnvs;
   dim3 grid((unsigned)std::min<int64_t>(nblk, (int64_t)wpc * h->num_cus)), block(256);
-  size_t lds = quad_lds_bytes(h->g, false);
+  size_t lds = quad_lds_bytes(h->g, false, false);
   if (wpc < 4) lds = std::max(lds, (size_t)160 * 1024 / (wpc + 1) + 16);
   switch (wpc) {
     case 2: hipLaunchKernelGGL((pe_step_pipe<16, 6, 2>), grid, block, lds, s, a); break;
@@ -2655,7 +2671,7 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
   if (is_quad(h->variant)) {
     const int nw = h->quad_waves, epb = h->quad_epb;
     dim3 grid((unsigned)((h->n + epb - 1) / epb)), block(nw * 64);
-    size_t lds = quad_lds_bytes(h->g, h->tile_codes);
+    size_t lds = quad_lds_bytes(h->g, h->tile_codes, h->variant >= V_QUAD_RT_1W);
     if (h->lds_floor > lds) lds = h->lds_floor;  // diagnostics: caps workgroups per CU
 #define PE_QUAD(CC, RR, OW)                                                                 \
   if (h->tile_codes)                                                                        \
@@ -3035,7 +3051,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
 #ifdef PE_DEBUG_KNOBS
   if (const char* sg = std::getenv("PE_STAGGER")) h->stagger = std::atoi(sg);
 #endif
-  if (is_quad(h->variant) && quad_lds_bytes(g, h->tile_codes) > 160 * 1024)
+  if (is_quad(h->variant) && quad_lds_bytes(g, h->tile_codes, h->variant >= V_QUAD_RT_1W) > 160 * 1024)
     h->variant = h->variant <= V_QUAD_C64R6 ? h->variant - (V_QUAD_C16R6_1W - V_C16R6_1W) : V_GENERIC;
 #ifdef PE_DEBUG_KNOBS
   if (const char* kenv = std::getenv("PE_STEP_KERNEL"))
