@@ -103,10 +103,13 @@ typedef struct pe_config {
                                    per value, every value is one of < 256 table floats):
                                    pe_step_codes writes them (5C+27 B per env instead of
                                    4(5C+27)), pe_expand_obs_codes turns them into floats.
-                                   Sector-kernel geometries with a byte-coded tile only
-                                   (C = 16 / R = 6 with G <= 20, C = 64 / R = 6); pe_create
-                                   fails with PE_ERR_ARG elsewhere.  pe_step still writes
-                                   f32 obs on such a handle.  0 (default): off          */
+                                   Geometries whose step kernel is a sector kernel that
+                                   can hold a byte-coded tile: C = 16 / R = 6 with G <= 20,
+                                   C = 64 / R = 6, and every geometry of the runtime-(C, R)
+                                   sector kernel (4 <= C <= 64, 2 <= R <= 14, no compile-
+                                   time kernel); pe_create fails with PE_ERR_ARG elsewhere.
+                                   pe_step still writes f32 obs on such a handle.
+                                   0 (default): off                                     */
     int32_t reserved[3];
 } pe_config;
 

@@ -1630,7 +1630,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
 }
 
 #ifdef PE_DEBUG_KNOBS  // the persistent pipelined kernel: a debug-build A/B only (measured slower)
-#include "pe_pipe.hpp"
+#include "../../tools/diag/pe_pipe.hpp"  // (the closed A/B kernel lives with the diagnostics)
 #endif
 
 // ---------------------------------------------------------------- pe_step_wave
@@ -2673,6 +2673,7 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
     dim3 grid((unsigned)((h->n + epb - 1) / epb)), block(nw * 64);
     size_t lds = quad_lds_bytes(h->g, h->tile_codes, h->variant >= V_QUAD_RT_1W);
     if (h->lds_floor > lds) lds = h->lds_floor;  // diagnostics: caps workgroups per CU
+#ifdef PE_DEBUG_KNOBS  // 8 waves of 64 envs: the PE_QUAD_WAVES=8 A/B only (they spill: never in the product)
 #define PE_QUAD(CC, RR, OW)                                                                 \
   if (h->tile_codes)                                                                        \
     hipLaunchKernelGGL((pe_step_quad<CC, RR, OW, 4, true>), grid, block, lds, s, a);        \
@@ -2680,6 +2681,13 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((pe_step_quad<CC, RR, OW, 8>), grid, block, lds, s, a);              \
   else                                                                                      \
     hipLaunchKernelGGL((pe_step_quad<CC, RR, OW, 4>), grid, block, lds, s, a);
+#else
+#define PE_QUAD(CC, RR, OW)                                                                 \
+  if (h->tile_codes)                                                                        \
+    hipLaunchKernelGGL((pe_step_quad<CC, RR, OW, 4, true>), grid, block, lds, s, a);        \
+  else                                                                                      \
+    hipLaunchKernelGGL((pe_step_quad<CC, RR, OW, 4>), grid, block, lds, s, a);
+#endif
 #define PE_QUAD4(CC, RR, OW) hipLaunchKernelGGL((pe_step_quad<CC, RR, OW, 4>), grid, block, lds, s, a);
     switch (h->variant) {
       case V_QUAD_C16R6_1W:
@@ -2693,7 +2701,11 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
           PE_QUAD(16, 6, true);
         break;
       case V_QUAD_C16R6: PE_QUAD4(16, 6, false); break;
-      case V_QUAD_C64R6: PE_QUAD(64, 6, false); break;
+#ifdef PE_DEBUG_KNOBS
+      case V_QUAD_C64R6: PE_QUAD(64, 6, false); break;  // (PE_TILE_CODES=0: the f32-tile A/B)
+#else
+      case V_QUAD_C64R6: hipLaunchKernelGGL((pe_step_quad<64, 6, false, 4, true>), grid, block, lds, s, a); break;
+#endif
       case V_QUAD_C10R2_1W: PE_QUAD4(10, 2, true); break;
       case V_QUAD_C10R2: PE_QUAD4(10, 2, false); break;
       case V_QUAD_C16R4_1W: PE_QUAD4(16, 4, true); break;
@@ -3100,6 +3112,9 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   if (h->quad_epb != kQuadEnvs) {
     std::snprintf(h->kname_buf, sizeof(h->kname_buf), "%.*s%s,E%d>", (int)std::strlen(h->kname) - 1, h->kname,
                   h->quad_waves == 8 ? ",W8" : "", h->quad_epb);
+    h->kname = h->kname_buf;
+  } else if (h->tile_codes) {  // the byte-coded tile instantiation (pe_step_quad<..., BT = true>)
+    std::snprintf(h->kname_buf, sizeof(h->kname_buf), "%.*s,bytetile>", (int)std::strlen(h->kname) - 1, h->kname);
     h->kname = h->kname_buf;
   }
   // explicit reset-path tuning (pe_config.coop_max_done; -1: the choice above) --

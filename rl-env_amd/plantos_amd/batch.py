@@ -154,6 +154,17 @@ class PlantOSBatch:
             raise ValueError(f"src must be a contiguous uint8 device tensor of {blocks} x {stride} bytes")
         if obs is None:
             obs = torch.empty((blocks * n, D), dtype=torch.float32, device=self.device)
+        # the kernel writes blocks*n rows of D floats and blocks*n per-env values through raw
+        # pointers: every output must be exactly that, on this batch's device
+        rows = blocks * n
+        for name, t, dt, shape in (("obs", obs, torch.float32, (rows, D)), ("reward", reward, torch.float32, (rows,)),
+                                   ("terminated", terminated, torch.uint8, (rows,)),
+                                   ("truncated", truncated, torch.uint8, (rows,))):
+            if t is None:
+                continue
+            if not (type(t) is torch.Tensor and t.dtype is dt and t.is_cuda and t.get_device() == self._dev_index
+                    and t.is_contiguous() and tuple(t.shape) == shape):
+                raise ValueError(f"{name} must be a contiguous {dt} tensor of shape {shape} on {self.device}")
         with torch.cuda.device(self.device):
             C.check(C.lib().pe_expand_obs_codes(self.handle, int(blocks), n, _ptr(src), stride, _ptr(obs), _ptr(reward),
                                                 _ptr(terminated), _ptr(truncated), self._stream()),

@@ -34,6 +34,8 @@ class ShardedPlantOS:
     """
 
     def __init__(self, envs_per_rank, seed=0, batch_factory=None, group=None, codes=False, **cfg):
+        if "obs_codes" in cfg:
+            raise TypeError("ShardedPlantOS: pass codes=True, not obs_codes (the shard's unpack follows `codes`)")
         self.group = group
         self.codes = bool(codes)
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -49,10 +51,11 @@ class ShardedPlantOS:
             batch_factory = lambda n, **kw: PlantOSBatch(n, device=dev, **cfg, **kw)  # noqa: E731
         extra = {"obs_codes": True} if self.codes else {}
         self.batch = batch_factory(self.n, env_id_offset=lo, seed=seed, **extra)
+        # the io layout the batch actually writes (a factory may set it regardless of `codes`)
+        self.codes = bool(getattr(self.batch, "obs_codes", False))
         self._slots = None
         self._last_io = None  # the buffer the latest step wrote (None: the batch's own io)
         self._gbuf = None     # root: gather_outputs' [W, io_bytes] buffer
-        self._out = None      # root, codes: the expanded global outputs (reused every step)
 
     @property
     def device(self):
@@ -86,22 +89,17 @@ class ShardedPlantOS:
     def unpack(self, flats, out=None):
         """The W ranks' packed buffers (rank order: ``gathered(slot)``'s [W, io_bytes]
         rows) as the global (obs f32 [W*n, D], reward f32 [W*n], terminated u8,
-        truncated u8).  codes: ONE expansion kernel writes them into `out` (four
-        contiguous tensors; default: buffers this object owns and reuses, valid until
-        the next unpack); otherwise the f32 parts are concatenated."""
+        truncated u8).  codes: ONE expansion kernel writes them into fresh tensors, or
+        into `out` (four contiguous tensors the caller owns and may reuse: an explicit
+        opt-in, so that both modes hand out tensors the next unpack never overwrites);
+        otherwise the f32 parts are concatenated."""
         n = self.n
         D = self.batch.obs_dim
         if self.codes:
             src = flats if isinstance(flats, torch.Tensor) else torch.stack(list(flats))
             W = src.shape[0] if src.dim() == 2 else 1
             if out is None:
-                if self._out is None or self._out[0].shape[0] != W * n:
-                    dev = src.device
-                    self._out = (torch.empty((W * n, D), dtype=torch.float32, device=dev),
-                                 torch.empty(W * n, dtype=torch.float32, device=dev),
-                                 torch.empty(W * n, dtype=torch.uint8, device=dev),
-                                 torch.empty(W * n, dtype=torch.uint8, device=dev))
-                out = self._out
+                out = self.new_outputs(W)
             self.batch.expand_codes(src.reshape(-1), W, *out)
             return out
         sizes = (4 * n * D, 4 * n, n, n)
@@ -113,6 +111,15 @@ class ShardedPlantOS:
                 off += sz
         obs = torch.cat(parts[0]).view(torch.float32).view(-1, D)
         return obs, torch.cat(parts[1]).view(torch.float32), torch.cat(parts[2]), torch.cat(parts[3])
+
+    def new_outputs(self, W=None):
+        """Four contiguous tensors for the expanded global outputs of W ranks (default:
+        this job's world): obs f32 [W*n, D], reward f32, terminated u8, truncated u8 --
+        the `out` a consumer that reuses its buffers passes to unpack."""
+        W = self.world if W is None else int(W)
+        n, D, dev = self.n, self.batch.obs_dim, self.device
+        return (torch.empty((W * n, D), dtype=torch.float32, device=dev), torch.empty(W * n, dtype=torch.float32, device=dev),
+                torch.empty(W * n, dtype=torch.uint8, device=dev), torch.empty(W * n, dtype=torch.uint8, device=dev))
 
     def gather_outputs(self, root=0):
         """(obs, reward, terminated, truncated) of all ranks, concatenated in global

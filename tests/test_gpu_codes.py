@@ -108,6 +108,34 @@ def test_expand_many_blocks_is_one_gather_buffer():
         b.close()
 
 
+def test_expand_codes_rejects_bad_outputs():
+    """every caller-supplied output of expand_codes is checked before the raw-pointer
+    launch: wrong shape (rows of one block for two), dtype, contiguity or device"""
+    cfg = CFG["g20"]
+    n = 128
+    b = make(cfg, n, obs_codes=True)
+    D = b.obs_dim
+    src = torch.zeros(2 * b.io_bytes(), dtype=torch.uint8, device="cuda:0")
+    f32, u8 = torch.float32, torch.uint8
+    good = dict(obs=torch.empty((2 * n, D), dtype=f32, device="cuda:0"),
+                reward=torch.empty(2 * n, dtype=f32, device="cuda:0"),
+                terminated=torch.empty(2 * n, dtype=u8, device="cuda:0"),
+                truncated=torch.empty(2 * n, dtype=u8, device="cuda:0"))
+    b.expand_codes(src, 2, **good)  # the right shapes pass
+    bad = [("obs", torch.empty((n, D), dtype=f32, device="cuda:0")),
+           ("obs", torch.empty((2 * n, D + 1), dtype=f32, device="cuda:0")[:, :D]),
+           ("obs", torch.empty((2 * n, D), dtype=f32)),
+           ("reward", torch.empty(2 * n, dtype=torch.float64, device="cuda:0")),
+           ("terminated", torch.empty(2 * n, dtype=f32, device="cuda:0")),
+           ("truncated", torch.empty(n, dtype=u8, device="cuda:0"))]
+    for name, t in bad:
+        kw = dict(good)
+        kw[name] = t
+        with pytest.raises(ValueError):
+            b.expand_codes(src, 2, **kw)
+    b.close()
+
+
 def test_sharded_codes_one_gpu_no_process_group():
     """ShardedPlantOS(codes=True) without torch.distributed: step_gather / gathered /
     unpack on one GPU equal the f32 batch of the same ids"""

@@ -172,6 +172,34 @@ def test_no_process_group():
                 assert sh.gathered(k).data_ptr() == sh._slots[k].data_ptr()
 
 
+def test_codes_follow_the_batch_and_unpack_owns_nothing():
+    """the shard's unpack layout follows the batch it built (a factory that writes codes
+    regardless of `codes=`), obs_codes in cfg is refused, and a code-mode unpack returns
+    fresh tensors (a later unpack never overwrites an earlier result) unless `out` is
+    passed -- the same ownership as the f32 path's concatenation"""
+    _paths()
+    import pytest
+    from plantos_amd.shard import ShardedPlantOS
+    assert not dist.is_initialized()
+    sh = _shard(6, False)
+    base = sh.batch.__class__
+    forced = ShardedPlantOS(6, seed=9, batch_factory=lambda n_, **kw: base(n_, **dict(kw, obs_codes=True)))
+    assert forced.codes and forced.batch.obs_codes
+    with pytest.raises(TypeError):
+        ShardedPlantOS(6, seed=9, batch_factory=lambda n_, **kw: base(n_, **kw), obs_codes=True)
+    sh = _shard(6, True)
+    k = sh.step_gather(torch.zeros(6, dtype=torch.int64))
+    first = sh.unpack(sh.gathered(k))
+    keep = [x.clone() for x in first]
+    k2 = sh.step_gather(torch.full((6,), 4, dtype=torch.int64))
+    second = sh.unpack(sh.gathered(k2))
+    assert all(a.data_ptr() != b.data_ptr() for a, b in zip(first, second))
+    assert all(torch.equal(a, b) for a, b in zip(first, keep))
+    out = sh.new_outputs()
+    res = sh.unpack(sh.gathered(k2), out=out)
+    assert all(r is o for r, o in zip(res, out)) and all(torch.equal(a, b) for a, b in zip(res, second))
+
+
 def test_code_roundtrip_on_oracle_obs():
     """codes.py: expand(encode(obs)) == obs bit for bit over oracle rollouts of two
     geometries (incl. auto-reset obs), and the code io layout is 16-B padded"""
