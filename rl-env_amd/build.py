@@ -22,7 +22,7 @@ SRC_HOST = os.path.join(HERE, "csrc", "pe_pystream.cpp")
 SRC_MCTS = os.path.join(HERE, "csrc", "pe_mcts.hip")
 SOURCES = [SRC, SRC_MCTS, SRC_HOST]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", f) for f in
-                  ("pe_device.hpp", "pe_fast.hpp", "pe_quad.hpp", "pe_coop.hpp", "pe_handle.hpp")] + [
+                  ("pe_device.hpp", "pe_fast.hpp", "pe_quad.hpp", "pe_coop.hpp", "pe_handle.hpp", "pe_far.hpp")] + [
     os.path.join(REPO, "include", "plantos_batch.h"), os.path.join(HERE, "tools_gen_lidar.py")]
 OUT = os.path.join(HERE, "plantos_amd", "libplantos_hip.so")
 OBJ_DIR = os.path.join(REPO, "build", "obj")

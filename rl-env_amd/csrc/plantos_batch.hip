@@ -533,6 +533,12 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
 #ifndef PE_QUAD_TILE_BUF
 #define PE_QUAD_TILE_BUF 0  // sector kernel's f32 tile: asm sc1 stores (0); A/B: buffer stores (1, 2)
 #endif
+#ifndef PE_BT_DV
+#define PE_BT_DV 1  // the byte-coded C16R6 kernel defers its overflow writes as the f32 one (A/B: 0)
+#endif
+#ifndef PE_BT_STAGE_MIN_C
+#define PE_BT_STAGE_MIN_C 64  // byte-coded kernels stage the predicted record by LDS-DMA from this C on (A/B: 0)
+#endif
 #ifndef PE_STAGGER_GROUPS
 #define PE_STAGGER_GROUPS 4  // sector kernel: the grid's start-delay groups (A/B: -DPE_STAGGER_GROUPS=n)
 #endif
@@ -1244,7 +1250,9 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // only -- measured faster there (9.66 -> 9.52 us), slower in the constructor default's
   // multi-word C10R2 kernel (8.22 -> 8.69) and the 16-env small-batch shape (4.44 -> 4.61),
   // profiles/r4q/, r4v/
-  constexpr bool DV = C == 16 && R == 6 && ONEWORD && NW == 4 && !BT && EPB == kQuadEnvs;
+  // (round 5: the byte-coded twin of the headline kernel too -- config 5's codes step, A/B
+  // PE_BT_DV=0)
+  constexpr bool DV = C == 16 && R == 6 && ONEWORD && NW == 4 && (PE_BT_DV || !BT) && EPB == kQuadEnvs;
   const uint32_t vp0 = DV ? st.vpend[wv == CW || wv == 0 ? ec : 0] : 0u;  // (wave 0 applies, CW stores)
   // (Tried: the loader env's position by a bpermute from lane le of the wave instead of
   // this load -- 64x64 24.5 -> 25.2 us, 25x25 desync +0.4 us, the headline unchanged;
@@ -1297,7 +1305,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // around a possibly outstanding LDS-DMA (a vmcnt(0) at the next use of any load
   // result) serialize round 2 in every block (9.39 -> 10.0 us, desync 11.52 -> 12.29).
   float* stage = smem + tail_off + (RT ? quad_rtab_floats(Cr, Rr) : 0);
-  const bool stage_ok = BT && a.pf.scal && quad_coop(a, 1) && e0 + EPB <= a.n;  // full block: every lane live
+  // (C >= PE_BT_STAGE_MIN_C only: the byte-coded C16 kernel -- config 5's codes step --
+  // pays the same round-2 serialization as the f32 one would)
+  const bool stage_ok = BT && CM >= PE_BT_STAGE_MIN_C && a.pf.scal && quad_coop(a, 1) &&
+                        e0 + EPB <= a.n;  // full block: every lane live
   const bool stage_info = !st.cur && a.tinfo && pf_stage_info_fits(g.G, g.WPR, (int)a.pf.ostride);
   // (issued right after round 2's own loads: hipcc drains every memory op in flight
   // before the first use of a load result while an LDS-DMA is outstanding, so issued
@@ -1628,6 +1639,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
 #endif
   PE_STAMP(7);
 }
+
+#include "pe_far.hpp"  // pe_step_far<C, R>: the sector kernel of long LIDAR ranges (R > 14)
 
 #ifdef PE_DEBUG_KNOBS  // the persistent pipelined kernel: a debug-build A/B only (measured slower)
 #include "../../tools/diag/pe_pipe.hpp"  // (the closed A/B kernel lives with the diagnostics)
@@ -2504,30 +2517,48 @@ __global__ void pe_synth_kernel(int n, uint64_t seed, uint32_t env_off, uint32_t
 // f32 | terminated | truncated, block b at src + b * stride) -> contiguous f32 obs
 // (+ the other outputs).  Grid: (x: 16-B output chunks, y: block); one u32 of 4 codes
 // per thread through the LDS code table, one 16-B store.
+constexpr int kExpandPer = 4;  // 4-code groups per thread (the table build amortized over 4 of them)
 __global__ __launch_bounds__(256) void pe_expand_codes_kernel(const Tables* tab, int R, int G, int D, int rows,
                                                               const uint8_t* src, int64_t stride, float* obs,
                                                               float* rew, uint8_t* te, uint8_t* tr) {
   __shared__ float ctab[256];
   ctab[threadIdx.x] = obs_code_value(tab, R, G, (int)threadIdx.x);
-  __syncthreads();
   const int b = blockIdx.y;
   const uint8_t* sb = src + (int64_t)b * stride;
   const int64_t nc = (int64_t)rows * D;  // codes per block
   float* ob = obs + (int64_t)b * nc;
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 4-code group
+  // a workgroup expands 256 * kExpandPer consecutive 4-code groups; thread t the groups
+  // g0 + t + 256 j (each load and each 16-B store instruction contiguous over the wave),
+  // every code word loaded before the table barrier
+  const int64_t g0 = (int64_t)blockIdx.x * 256 * kExpandPer + threadIdx.x;
   if ((nc & 3) == 0) {
-    if (4 * k < nc) {
-      const uint32_t c = *reinterpret_cast<const uint32_t*>(sb + 4 * k);
-      float4 v;
-      v.x = ctab[c & 255u];
-      v.y = ctab[(c >> 8) & 255u];
-      v.z = ctab[(c >> 16) & 255u];
-      v.w = ctab[c >> 24];
-      *reinterpret_cast<float4*>(ob + 4 * k) = v;
+    uint32_t c[kExpandPer];
+#pragma unroll
+    for (int j = 0; j < kExpandPer; ++j) {
+      const int64_t k = g0 + 256 * j;
+      c[j] = 4 * k < nc ? *reinterpret_cast<const uint32_t*>(sb + 4 * k) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kExpandPer; ++j) {
+      const int64_t k = g0 + 256 * j;
+      if (4 * k < nc) {
+        float4 v;
+        v.x = ctab[c[j] & 255u];
+        v.y = ctab[(c[j] >> 8) & 255u];
+        v.z = ctab[(c[j] >> 16) & 255u];
+        v.w = ctab[c[j] >> 24];
+        *reinterpret_cast<float4*>(ob + 4 * k) = v;
+      }
     }
   } else {
-    for (int64_t j = 4 * k; j < 4 * k + 4 && j < nc; ++j) ob[j] = ctab[sb[j]];
+    __syncthreads();
+    for (int j = 0; j < kExpandPer; ++j) {
+      const int64_t k = g0 + 256 * j;
+      for (int64_t i = 4 * k; i < 4 * k + 4 && i < nc; ++i) ob[i] = ctab[sb[i]];
+    }
   }
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;  // the per-env outputs below
   // the per-env outputs: one env per thread of the first ceil(rows / 256) workgroups
   if (k < rows) {
     const int64_t ro = (nc + 15) & ~(int64_t)15;
@@ -2627,7 +2658,8 @@ enum Variant {
   V_QUAD_C16R6_1W = 4, V_QUAD_C16R6 = 5, V_QUAD_C64R6 = 6,
   V_QUAD_C10R2_1W = 7, V_QUAD_C10R2 = 8,  // plantos_env.py:25-26 constructor default (G=21: multi-word)
   V_QUAD_C16R4_1W = 9, V_QUAD_C16R4 = 10,  // test_environment.py:24 (G=15, C=16, R=4)
-  V_QUAD_RT_1W = 11, V_QUAD_RT = 12        // runtime (C, R): every other geometry with C <= 64, 2 <= R <= 14
+  V_QUAD_RT_1W = 11, V_QUAD_RT = 12,       // runtime (C, R): every other geometry with C <= 64, 2 <= R <= 14
+  V_FAR_C64R32 = 13                         // pe_step_far<64, 32>: SURVEY §8(d)'s R = 32 stress variant
 };
 
 // the prefetched records' obs row stride (bytes; pe_device.hpp Prefetch)
@@ -2644,6 +2676,13 @@ size_t quad_lds_bytes(const Geo& g, bool codes, bool rt) {
 }
 
 bool is_quad(int v) { return v >= V_QUAD_C16R6_1W; }
+bool is_far(int v) { return v == V_FAR_C64R32; }
+
+// the step kernel's dynamic LDS (sector kernels)
+size_t step_lds_bytes(const Geo& g, int variant, bool codes) {
+  if (is_far(variant)) return sizeof(float) * (size_t)far_lds_floats(g.G, g.WPR, g.C, g.R);
+  return quad_lds_bytes(g, codes, variant >= V_QUAD_RT_1W);
+}
 
 #ifdef PE_DEBUG_KNOBS
 // the persistent pipelined kernel's grid and LDS: min(blocks, WPC per CU); the LDS
@@ -2668,10 +2707,15 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
 #ifdef PE_DEBUG_KNOBS
   if (h->pipe_wpc > 0) return launch_pipe(h, a, s);
 #endif
-  if (is_quad(h->variant)) {
+  if (is_far(h->variant)) {
+    dim3 grid((unsigned)((h->n + kQuadEnvs - 1) / kQuadEnvs)), block(64 * kFarWaves);
+    size_t lds = step_lds_bytes(h->g, h->variant, true);
+    if (h->lds_floor > lds) lds = h->lds_floor;  // diagnostics: caps workgroups per CU
+    hipLaunchKernelGGL((pe_step_far<64, 32>), grid, block, lds, s, a);
+  } else if (is_quad(h->variant)) {
     const int nw = h->quad_waves, epb = h->quad_epb;
     dim3 grid((unsigned)((h->n + epb - 1) / epb)), block(nw * 64);
-    size_t lds = quad_lds_bytes(h->g, h->tile_codes, h->variant >= V_QUAD_RT_1W);
+    size_t lds = step_lds_bytes(h->g, h->variant, h->tile_codes);
     if (h->lds_floor > lds) lds = h->lds_floor;  // diagnostics: caps workgroups per CU
 #ifdef PE_DEBUG_KNOBS  // 8 waves of 64 envs: the PE_QUAD_WAVES=8 A/B only (they spill: never in the product)
 #define PE_QUAD(CC, RR, OW)                                                                 \
@@ -2825,6 +2869,7 @@ const char* variant_name(int v) {
     case V_QUAD_C16R4: return "pe_step_quad<C16,R4>";
     case V_QUAD_RT_1W: return "pe_step_quad<runtime C,R,1word>";
     case V_QUAD_RT: return "pe_step_quad<runtime C,R>";
+    case V_FAR_C64R32: return "pe_step_far<C64,R32>";
     default: return "pe_step_wave";
   }
 }
@@ -3018,6 +3063,10 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   // sector kernels of the other specialized geometries (4 waves; no lane-kernel twin)
   if (!lane_kernels && C == 10 && R == 2 && table_matches<10, 2>(ldx, ldy)) h->variant = V_QUAD_C10R2_1W;
   if (!lane_kernels && C == 16 && R == 4 && table_matches<16, 4>(ldx, ldy)) h->variant = V_QUAD_C16R4_1W;
+  // R > 14 with a compile-time table: the far sector kernel (its rows and the auto-reset
+  // path's are kCoopWPR words: 96 < G + 2R <= 128)
+  if (!lane_kernels && C == 64 && R == 32 && g.WPR == kCoopWPR && table_matches<64, 32>(ldx, ldy))
+    h->variant = V_FAR_C64R32;
   // the one-word form (whole padded row in one u64) needs WPR == 1 and 16-B visit
   // rows (NW == 4: G <= 20); otherwise the multi-word (funnel-shifted) form
   const bool oneword = g.WPR == 1 && g.NW == 4;
@@ -3033,7 +3082,8 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   if (h->variant == V_QUAD_C16R6_1W && g.NW != 4) h->variant = V_C16R6_1W;  // needs 16-B visit rows
   // byte-coded obs tile where the f32 tile limits the sector kernel's occupancy
   // (C = 64: 89 KB -> 22 KB of LDS per workgroup)
-  h->tile_codes = h->variant == V_QUAD_C64R6 || (is_quad(h->variant) && h->variant >= V_QUAD_RT_1W && C > kRtCMax)
+  h->tile_codes = h->variant == V_QUAD_C64R6 || is_far(h->variant) ||
+                          (is_quad(h->variant) && h->variant >= V_QUAD_RT_1W && C > kRtCMax)
                       ? 1 : 0;
 #ifdef PE_DEBUG_KNOBS
   if (const char* tc = std::getenv("PE_TILE_CODES"))
@@ -3043,7 +3093,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   h->obs_codes = c->obs_codes ? 1 : 0;
   if (h->obs_codes) {
     if (!(h->variant == V_QUAD_C16R6_1W || h->variant == V_QUAD_C64R6 || h->variant == V_QUAD_RT_1W ||
-          h->variant == V_QUAD_RT)) {
+          h->variant == V_QUAD_RT || is_far(h->variant))) {
       delete[] ldx;
       delete[] ldy;
       delete h;
@@ -3063,7 +3113,7 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
 #ifdef PE_DEBUG_KNOBS
   if (const char* sg = std::getenv("PE_STAGGER")) h->stagger = std::atoi(sg);
 #endif
-  if (is_quad(h->variant) && quad_lds_bytes(g, h->tile_codes, h->variant >= V_QUAD_RT_1W) > 160 * 1024)
+  if (is_quad(h->variant) && step_lds_bytes(g, h->variant, h->tile_codes) > 160 * 1024)
     h->variant = h->variant <= V_QUAD_C64R6 ? h->variant - (V_QUAD_C16R6_1W - V_C16R6_1W) : V_GENERIC;
 #ifdef PE_DEBUG_KNOBS
   if (const char* kenv = std::getenv("PE_STEP_KERNEL"))
@@ -3439,7 +3489,9 @@ int pe_expand_obs_codes(const pe_handle* h, int32_t blocks, int32_t rows, const 
   DeviceGuard dg(h);
   if (dg.rc) return dg.rc;
   const int64_t groups = ((int64_t)rows * h->g.D + 3) / 4;
-  dim3 grid((unsigned)((groups + 255) / 256), (unsigned)blocks), block(256);
+  // kExpandPer groups per thread; the per-env outputs need a thread per env
+  const int64_t gx = std::max((groups + 256 * kExpandPer - 1) / (256 * kExpandPer), ((int64_t)rows + 255) / 256);
+  dim3 grid((unsigned)gx, (unsigned)blocks), block(256);
   hipLaunchKernelGGL(pe_expand_codes_kernel, grid, block, 0, static_cast<hipStream_t>(stream), h->st.tab, h->g.R,
                      h->g.G, h->g.D, rows, src, src_stride, obs, reward, terminated, truncated);
   PE_HIP(hipGetLastError());

@@ -24,7 +24,7 @@ CFG = {
     "g25": (25, 10, 12, 6, 16),   # the multi-word C16 sector kernel (train_mcts's grid)
     "g15": (15, 6, 8, 4, 16),     # one-word C16R4 sector kernel (test_environment.py:24)
     "g12r2": (12, 4, 6, 2, 10),   # one-word C10R2
-    "g64r32": (64, 100, 120, 32, 64),  # the one-wave-per-env kernel (long rays)
+    "g64r32": (64, 100, 120, 32, 64),  # the far sector kernel (long rays, pe_step_far)
     "g30r2": (30, 12, 40, 2, 10),  # multi-word C10R2
     "g16c40": (16, 6, 8, 5, 40),   # C > 32: the runtime sector kernel, byte-coded tile
     "g40c48": (40, 100, 120, 8, 48),  # the same, multi-word rows (bench geometry)

@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 CFG = {
     "g20": (20, 10, 12, 6, 16),       # pe_step_quad<C16,R6,1word> (f32 tile, prefetched records)
     "g64": (64, 100, 120, 6, 64),     # pe_step_quad<C64,R6> (byte-coded tile, LDS-DMA staged records)
-    "g64r32": (64, 100, 120, 32, 64),  # pe_step_wave
+    "g64r32": (64, 100, 120, 32, 64),  # pe_step_far
 }
 
 

@@ -6,7 +6,9 @@ one-wave-per-env kernel (C > 64, R > 14 or R = 1) -- each against the oracle
 desynchronized so that auto-resets happen inside the window, the final state
 included.  Batch sizes are ragged (a partial last workgroup).  A second sweep covers
 33 <= C <= 64 (round 4: the byte-coded runtime sector kernel) and the byte-coded
-obs boundary (obs_codes) on runtime-sector geometries."""
+obs boundary (obs_codes) on runtime-sector geometries; a third (round 5) the long ranges
+R in {16, 20, 32}, C = 64 / R = 32 through the far sector kernel (pe_step_far) where it
+applies.  The verdict's R > 14 sweep case."""
 import numpy as np
 import pytest
 import torch
@@ -58,19 +60,29 @@ def _wide_geometries():
 
 GEOS = _geometries()
 WIDE = _wide_geometries()
+# long ranges (R > 14, round 5): C = 64 / R = 32 at G in [33, 64] runs the far sector
+# kernel (pe_step_far, compile-time rays, G + 2R in (96, 128]); R = 16 / 20 and G
+# outside that range the one-wave-per-env kernel
+FAR = [(64, 100, 120, 32, 64), (40, 30, 40, 32, 64), (33, 12, 20, 32, 64), (21, 8, 10, 32, 64),
+       (48, 40, 60, 16, 64), (24, 10, 12, 20, 16)]
+
+
+def _far_kernel(G, R, C):
+    return C == 64 and R == 32 and 96 < G + 2 * R <= 128
 
 
 def _ids(geos):
     return [f"G{g}P{p}O{o}R{r}C{c}" for g, p, o, r, c in geos]
 
 
-@pytest.mark.parametrize("cfg", GEOS + WIDE, ids=_ids(GEOS) + _ids(WIDE))
+@pytest.mark.parametrize("cfg", GEOS + WIDE + FAR, ids=_ids(GEOS) + _ids(WIDE) + _ids(FAR))
 def test_geometry_sweep_parity(cfg):
     _sweep(cfg, codes=False)
 
 
-# the byte-coded obs boundary on runtime-sector geometries (f32 and byte tiles)
-CODES = [g for g in GEOS if 4 <= g[4] <= 64 and 2 <= g[3] <= 14][:3] + WIDE[:3]
+# the byte-coded obs boundary on runtime-sector geometries (f32 and byte tiles) and the
+# far sector kernel
+CODES = [g for g in GEOS if 4 <= g[4] <= 64 and 2 <= g[3] <= 14][:3] + WIDE[:3] + FAR[:2]
 
 
 @pytest.mark.parametrize("cfg", CODES, ids=_ids(CODES))
@@ -87,6 +99,8 @@ def _sweep(cfg, codes):
     rt = 4 <= C <= 64 and 2 <= R <= 14
     if rt:  # (or a compile-time specialization of the same sector kernel)
         assert b.kernel_name.startswith("pe_step_quad"), b.kernel_name
+    elif _far_kernel(G, R, C):
+        assert b.kernel_name == "pe_step_far<C64,R32,bytetile>", b.kernel_name
     elif C > 64 or R > 14:
         assert b.kernel_name == "pe_step_wave", b.kernel_name
     f32 = torch.empty((n, b.obs_dim), dtype=torch.float32, device="cuda:0")

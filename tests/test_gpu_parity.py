@@ -36,7 +36,7 @@ CFG = {
 KERNELS = {
     "g20": "pe_step_quad<C16,R6,1word>", "g25": "pe_step_quad<C16,R6>", "g64": "pe_step_quad<C64,R6,bytetile>",
     "g21": "pe_step_quad<C10,R2>", "g12r2": "pe_step_quad<C10,R2,1word>", "g30r2": "pe_step_quad<C10,R2>", "g15": "pe_step_quad<C16,R4,1word>",
-    "g25r4": "pe_step_quad<C16,R4>", "g64r32": "pe_step_wave", "g7": "pe_step_quad<runtime C,R,1word>",
+    "g25r4": "pe_step_quad<C16,R4>", "g64r32": "pe_step_far<C64,R32,bytetile>", "g7": "pe_step_quad<runtime C,R,1word>",
     "g32": "pe_step_quad<runtime C,R>", "g8r12": "pe_step_quad<runtime C,R,1word>", "g24c100": "pe_step_wave",
     "g8r20": "pe_step_wave", "g16c40": "pe_step_quad<runtime C,R,1word,bytetile>",
 }

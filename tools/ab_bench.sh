@@ -15,7 +15,7 @@ for r in $(seq 1 $ROUNDS); do
     IFS=, read -r LP ENVS <<< "$L"   # "path[,VAR=VAL ...]" (space-separated env assignments)
     if [ "$LP" = tree ]; then unset PLANTOS_HIP_LIB; else export PLANTOS_HIP_LIB=$LP; fi
     env ${ENVS:-} timeout -k 10 120 python bench.py --no-cpu-baseline $ARGS > gpurun_out/ab_one.json 2> gpurun_out/ab_one.err
-    python3 -c "import json,sys; d=json.load(open('gpurun_out/ab_one.json')); print(json.dumps({'lib': sys.argv[1], 'round': int(sys.argv[2]), 'kernel_us': d['roofline']['kernel_ms']*1e3, 'wall_us': d['ms_per_step']*1e3, 'desync_us': d.get('desync', {}).get('us_per_step'), 'value': d['value'], 'kernel': d['config']['kernel']}))" "$L" "$r" >> $OUT
+    python3 -c "import json,sys; d=json.load(open('gpurun_out/ab_one.json')); rf=d['roofline']; g=d.get('gather', {}); print(json.dumps({'lib': sys.argv[1], 'round': int(sys.argv[2]), 'kernel_us': rf['kernel_us_window'], 'events_us': rf['kernel_us_events'], 'wall_us': d['ms_per_step']*1e3, 'desync_us': d.get('desync', {}).get('us_per_step'), 'gather_us': g.get('us_per_step'), 'gather_step_us': g.get('step_us'), 'expand_us': g.get('expand_us'), 'value': d['value'], 'kernel': d['config']['kernel']}))" "$L" "$r" >> $OUT
   done
 done
 unset PLANTOS_HIP_LIB

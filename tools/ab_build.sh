@@ -9,9 +9,11 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 SRC=$ROOT/build/ab/src_$NAME
 rm -rf "$SRC" && mkdir -p "$SRC"
 if [ "$REV" = WORKTREE ]; then
-  mkdir -p "$SRC/rl-env_amd" && cp -r "$ROOT/rl-env_amd/csrc" "$SRC/rl-env_amd/" && cp -r "$ROOT/include" "$SRC/"
+  mkdir -p "$SRC/rl-env_amd" "$SRC/tools/diag" && cp -r "$ROOT/rl-env_amd/csrc" "$SRC/rl-env_amd/" && cp -r "$ROOT/include" "$SRC/"
+  cp "$ROOT/tools/diag/pe_pipe.hpp" "$SRC/tools/diag/"  # (the debug-only pipelined kernel)
 else
   git -C "$ROOT" archive "$REV" rl-env_amd/csrc include | tar -x -C "$SRC"
+  git -C "$ROOT" archive "$REV" tools/diag 2>/dev/null | tar -x -C "$SRC" || true
 fi
 if [ -n "${PATCH_PY:-}" ]; then (cd "$SRC" && python3 "$PATCH_PY"); fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -w -DPE_DEBUG_KNOBS ${EXTRA_FLAGS:-} \
