@@ -84,8 +84,13 @@ __host__ __device__ constexpr int far_tile_off(int G, int WPR, int C, int R) {
 __host__ __device__ constexpr int far_ctab_off(int G, int WPR, int C, int R) {
   return far_tile_off(G, WPR, C, R) + ((kQuadEnvs * (5 * C + 27) + 15) / 16) * 4;
 }
-__host__ __device__ constexpr int far_lds_floats(int G, int WPR, int C, int R) {
+// the commit wave's post-step scalars and return, parked in LDS for the done path
+// ([6][64] words: packed scalars x4, return x2) -- not held in registers across the rays
+__host__ __device__ constexpr int far_park_off(int G, int WPR, int C, int R) {
   return far_ctab_off(G, WPR, C, R) + 256;
+}
+__host__ __device__ constexpr int far_lds_floats(int G, int WPR, int C, int R) {
+  return far_park_off(G, WPR, C, R) + 6 * kQuadEnvs;
 }
 
 // Quadrant W's rays for this lane's env at the post-move position (xp, yp): first hit
@@ -372,14 +377,28 @@ __global__ __launch_bounds__(64 * kFarWaves, 4) void pe_step_far(StepArgs a) {
   const int xp = ok ? m.nx : s.x, yp = ok ? m.ny : s.y;
   const int dxv = xp - s.x;
   const uint32_t nib = n < 15u ? n + 1u : 15u;                         // :203
+  // Every wave's round-2 words consumed before the commit wave stores: its visit byte
+  // would otherwise reach a lagging wave's load of the same word (that wave then reads
+  // n + 1 and shows n + 2 at the slice centre -- seen with 4 workgroups per CU, never at
+  // one).  (The candidate slice rows and the rays' rows may see the new bytes: the slice
+  // centre is rebuilt from nib, the watered cell's fix is idempotent.)
+  asm volatile("s_barrier" ::"v"(vt), "v"(gt), "v"(gc) : "memory");
   uint8_t* row = rows + lane * D;
   bool done = false, wfix = false;
-  uint4 sp = make_uint4(0u, 0u, 0u, 0u);  // the commit wave's post-step scalars (its done path's)
+  uint32_t* park = reinterpret_cast<uint32_t*>(smem + far_park_off(g.G, g.WPR, C, R));
   if (live) {
     if (wv == CW) {
       done = far_commit(a, e, s, ret, m, ok, n, nib, watered, wet_hyd, xp, yp, gc, cbit, vt, tvp, vrow_t, gb32, rw32,
                         R, eo, en, cthr, wfix);
-      sp = pack(s);
+      // the post-step scalars and return for the done path, parked in LDS: in registers
+      // they were live across the rays (and spilled there)
+      const uint4 sp = pack(s);
+      park[lane] = sp.x;
+      park[64 + lane] = sp.y;
+      park[128 + lane] = sp.z;
+      park[192 + lane] = sp.w;
+      park[256 + lane] = (uint32_t)__double2loint(ret);
+      park[320 + lane] = (uint32_t)__double2hiint(ret);
     } else {
       // 5x5 slice rows lx = wv, wv + 3 (plantos_env.py:298-313) and the position (:294-296)
       const int vs = vo + 4 * (yp - m.ybv);  // bit of padded nibble column yp in the candidate words
@@ -423,8 +442,14 @@ __global__ __launch_bounds__(64 * kFarWaves, 4) void pe_step_far(StepArgs a) {
   const bool any_done = dmu != 0ull;
   const int ndone = __popcll(dmu);
   const int64_t valid = a.n - e0 < LS ? a.n - e0 : LS;
+  uint4 sp = make_uint4(0u, 0u, 0u, 0u);
   if (__builtin_expect(any_done, 0)) {
-    sp = far_done<C, R>(kernargs(), tile_off, lane, wv, e0, done, sp, ret, ndone, wfix, ctab);
+    double rv = 0.0;
+    if (wv == CW) {  // (the other waves' values are not used by the done path)
+      sp = make_uint4(park[lane], park[64 + lane], park[128 + lane], park[192 + lane]);
+      rv = __hiloint2double((int)park[320 + lane], (int)park[256 + lane]);
+    }
+    sp = far_done<C, R>(kernargs(), tile_off, lane, wv, e0, done, sp, rv, ndone, wfix, ctab);
   }
   if (wv == CW) __builtin_amdgcn_s_waitcnt(0x0F70);  // tracked vmcnt(0): no wait inside the store loop
   if (a.obs_codes)

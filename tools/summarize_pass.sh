@@ -14,7 +14,25 @@ for x in drv n4096 g25 g21 g15 g32 g64r32 g40c48; do cp $G/benchx_${x}_$T.json $
 cp $G/stats_$T/run_kernel_stats.csv $P/${T}_kernel_stats.csv
 cp $G/statsd_$T/run_kernel_stats.csv $P/${T}_kernel_stats_desync.csv
 cp $G/stats64_$T/run_kernel_stats.csv $P/${T}_kernel_stats_64.csv
-for x in n4096 g25 g64r32 g40c48; do cp $G/statsx_${x}_$T/run_kernel_stats.csv $P/${T}_kernel_stats_${x}.csv; done
+for x in n4096 g25 g64r32 g40c48 g32 gather; do cp $G/statsx_${x}_$T/run_kernel_stats.csv $P/${T}_kernel_stats_${x}.csv; done
+# the gather leg's kernel trace (the step into the slot, the expansion, the gaps between them)
+python3 - $G/statsx_gather_$T/run_kernel_trace.csv $P/${T}_gather_kernel_trace.csv <<'PY'
+import csv, sys
+rows = list(csv.DictReader(open(sys.argv[1])))
+keep = [r for r in rows if "bytetile" in r.get("Kernel_Name", "") or "expand" in r.get("Kernel_Name", "")
+        or "pe_step_quad<16, 6, true, 4, true" in r.get("Kernel_Name", "")][-400:]
+if keep:
+    w = csv.DictWriter(open(sys.argv[2], "w"), fieldnames=list(keep[0].keys()))
+    w.writeheader()
+    w.writerows(keep)
+PY
+# the step kernel's rocprof average per stats run, keyed by lib_sha + config (bench.py rocprof_kernel_ns)
+python3 tools/kstats_summary.py $P/kstats_${T}.json $P/${T}_kernel_stats.csv $G/stats_bench_$T.json
+python3 tools/kstats_summary.py $P/kstats_${T}_desync.json $P/${T}_kernel_stats_desync.csv $G/statsd_bench_$T.json
+python3 tools/kstats_summary.py $P/kstats_${T}_64.json $P/${T}_kernel_stats_64.csv $G/stats64_bench_$T.json
+for x in n4096 g25 g64r32 g40c48 g32; do
+  python3 tools/kstats_summary.py $P/kstats_${T}_$x.json $P/${T}_kernel_stats_$x.csv $G/statsx_${x}_$T.json
+done
 python3 tools/pmc_summary.py $T --fetch-dir pmcf_$T --write-dir pmcw_$T --bench-json $G/pmcf_$T.json \
   --stats-dir stats_$T > /dev/null
 python3 tools/pmc_summary.py $T --out-prefix pmc64 --fetch-dir pmcf64_$T --write-dir pmcw64_$T \
@@ -23,8 +41,8 @@ for x in g25 n4096; do
   python3 tools/pmc_summary.py $T --out-prefix pmc_$x --fetch-dir pmcx_${x}_FETCH_SIZE_$T \
     --write-dir pmcx_${x}_WRITE_SIZE_$T --bench-json $G/pmcx_${x}_FETCH_SIZE_$T.json --stats-dir statsx_${x}_$T > /dev/null
 done
-# the wave kernel's window span and visit rows are streamed reads too
-python3 tools/pmc_summary.py $T --out-prefix pmc_g64r32 --fetch-dir pmcx_g64r32_FETCH_SIZE_$T \
-  --write-dir pmcx_g64r32_WRITE_SIZE_$T --bench-json $G/pmcx_g64r32_FETCH_SIZE_$T.json \
-  --stats-dir statsx_g64r32_$T --streamed-bytes 1820 --kernel pe_step_wave > /dev/null
+for x in g64r32 g40c48 g32; do
+  python3 tools/pmc_summary.py $T --out-prefix pmc_$x --fetch-dir pmcx_${x}_FETCH_SIZE_$T \
+    --write-dir pmcx_${x}_WRITE_SIZE_$T --bench-json $G/pmcx_${x}_FETCH_SIZE_$T.json --stats-dir statsx_${x}_$T > /dev/null
+done
 ls -la $P/*_$T.json $P/${T}_* | wc -l
