@@ -36,9 +36,10 @@
 
 constexpr int kFarWaves = 4;
 #ifndef PE_FAR_ROW_BATCH
-#define PE_FAR_ROW_BATCH 9
+#define PE_FAR_ROW_BATCH 33  // one batch: the compiler's schedule (9: 55.1 us, 12: 54.3, 17: 54.6, 33: 53.7 at
+                             // 64x64/C64/R32, same box, profiles/r5f/, r5h/)
 #endif
-constexpr int kFarRowBatch = PE_FAR_ROW_BATCH;  // quadrant rows per load batch (33 rows at R = 32: 4 batches)
+constexpr int kFarRowBatch = PE_FAR_ROW_BATCH;  // quadrant rows per load batch
 constexpr int kFarRow32 = 2 * kCoopWPR;  // u32 words per padded grid row: the kernel takes G + 2R in (96, 128]
 
 template <int C, int R>
@@ -85,12 +86,22 @@ __host__ __device__ constexpr int far_ctab_off(int G, int WPR, int C, int R) {
   return far_tile_off(G, WPR, C, R) + ((kQuadEnvs * (5 * C + 27) + 15) / 16) * 4;
 }
 // the commit wave's post-step scalars and return, parked in LDS for the done path
-// ([6][64] words: packed scalars x4, return x2) -- not held in registers across the rays
+// ([6][64] words: packed scalars x4, return x2) -- not held in registers across the
+// rays.  In the tail of the done path's scratch: read back before the done path runs.
 __host__ __device__ constexpr int far_park_off(int G, int WPR, int C, int R) {
-  return far_ctab_off(G, WPR, C, R) + 256;
+  return far_tile_off(G, WPR, C, R) - 6 * kQuadEnvs;
 }
+// the single-done record's LDS-DMA staging region (pe_coop.hpp pf_stage_issue; the
+// byte-coded records' obs rows: 5C+27 codes rounded up to 16 B).  Not the env's current
+// rows for the terminal info: 5 LDS-DMA instructions instead of 3 were slower
+// (desynchronized 60.7 -> 61.4 us at 64x64/C64/R32, profiles/r5j/)
+__host__ __device__ constexpr int far_stage_units(int G, int WPR, int C) {
+  return pf_stage_units(G, WPR, ((5 * C + 27) + 15) & ~15, false);
+}
+__host__ __device__ constexpr int far_stage_off(int G, int WPR, int C, int R) { return far_ctab_off(G, WPR, C, R) + 256; }
 __host__ __device__ constexpr int far_lds_floats(int G, int WPR, int C, int R) {
-  return far_park_off(G, WPR, C, R) + 6 * kQuadEnvs;
+  // (whole 64-unit LDS-DMA instructions: every lane of the last one writes its unit)
+  return far_stage_off(G, WPR, C, R) + 4 * 64 * ((far_stage_units(G, WPR, C) + 63) / 64);
 }
 
 // Quadrant W's rays for this lane's env at the post-move position (xp, yp): first hit
@@ -284,14 +295,15 @@ __device__ __forceinline__ bool far_commit(const StepArgs& a, int64_t e, Scal& s
 // line: a call, so that its register demand is its own (spilled on entry, cold) instead of
 // the hot path's -- inlined, the values live into it spilled in the kernel's prologue.
 // ka: the kernel's argument segment, taken in the kernel body (a noinline callee's own
-// kernarg pointer is 0 on gfx950 / ROCm 7.2).
+// kernarg pointer is 0 on gfx950 / ROCm 7.2).  stage: the done env's prefetched record,
+// staged into LDS by LDS-DMA (or nullptr).
 template <int C, int R>
 __device__ __attribute__((noinline)) uint4 far_done(const void* ka, int tile_off, int lane, int wv, int64_t e0,
                                                     bool done, uint4 sp, double ret, int ndone, bool wfix,
-                                                    const float* ctab) {
+                                                    const float* ctab, const float* stage, bool stage_info) {
   constexpr int D = 5 * C + 27;
   return quad_done_path<kFarWaves, false, (D + 63) / 64, true>(ka, tile_off, C, R, lane, wv, kFarWaves - 1, e0, done,
-                                                               sp, ret, ndone, wfix, ctab);
+                                                               sp, ret, ndone, wfix, ctab, stage, stage_info);
 }
 
 template <int C, int R>
@@ -344,6 +356,21 @@ __global__ __launch_bounds__(64 * kFarWaves, 4) void pe_step_far(StepArgs a) {
   uint32_t* vrow_t = vbase + (int64_t)tx * g.NW;
   const int tvp = ty + 2;  // padded nibble column of the target
   const uint32_t vt = vrow_t[(4 * tvp) >> 5];
+  // A block whose only env to truncate this step is known from its step count (:177;
+  // ~6 % of the blocks of a desynchronized batch): the commit wave stages that env's
+  // prefetched record into LDS by LDS-DMA now, so that its auto-reset makes no memory
+  // round trip of its own (as pe_step_quad's byte-coded kernel; issued right after this
+  // round's loads, see there)
+  float* stage = smem + far_stage_off(g.G, g.WPR, C, R);
+  const bool stage_ok = a.pf.scal && quad_coop(a, 1) && e0 + LS <= a.n;  // full block: every lane live
+  constexpr bool stage_info = false;  // (see far_stage_units)
+  int npred = 0;
+  if (stage_ok) {
+    const uint64_t pm = __ballot(s.step + 1 >= a.rl.max_steps);
+    npred = __popcll(pm);
+    if (wv == CW && npred == 1)
+      pf_stage_issue(a.pf, st, g, e0 + (__ffsll((unsigned long long)pm) - 1), stage, lane, stage_info);
+  }
   const int vw0 = (4 * m.ybv) >> 5, vo = (4 * m.ybv) & 31;
   uint32_t cv[2][3][2];  // [slice row t][candidate k][word]
   if (wv != CW) {
@@ -422,6 +449,9 @@ __global__ __launch_bounds__(64 * kFarWaves, 4) void pe_step_far(StepArgs a) {
       }
     }
     // ---- round 3 + the rays of this wave's quadrant
+#if defined(PE_FAR_PROBE) && PE_FAR_PROBE == 1  // timing probe (wrong obs): no rays
+    if (false)
+#endif
     switch (wv) {
       case 0: far_sector<C, R, 0>(gb32, g.G, xp, yp, watered, row); break;
       case 1: far_sector<C, R, 1>(gb32, g.G, xp, yp, watered, row); break;
@@ -449,9 +479,14 @@ __global__ __launch_bounds__(64 * kFarWaves, 4) void pe_step_far(StepArgs a) {
       sp = make_uint4(park[lane], park[64 + lane], park[128 + lane], park[192 + lane]);
       rv = __hiloint2double((int)park[320 + lane], (int)park[256 + lane]);
     }
-    sp = far_done<C, R>(kernargs(), tile_off, lane, wv, e0, done, sp, rv, ndone, wfix, ctab);
+    const bool staged = stage_ok && npred == 1 && ndone == 1;  // then the done env is the predicted one
+    sp = far_done<C, R>(kernargs(), tile_off, lane, wv, e0, done, sp, rv, ndone, wfix, ctab, staged ? stage : nullptr,
+                        staged && stage_info);
   }
   if (wv == CW) __builtin_amdgcn_s_waitcnt(0x0F70);  // tracked vmcnt(0): no wait inside the store loop
+#if defined(PE_FAR_PROBE) && PE_FAR_PROBE == 2  // timing probe (no obs): no tile store
+  if (false)
+#endif
   if (a.obs_codes)
     store_tile_bytes(rows, a.obs_codes + e0 * D, (int)valid, D, (int)threadIdx.x, (int)blockDim.x);
   else
