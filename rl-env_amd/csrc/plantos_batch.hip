@@ -633,6 +633,23 @@ __device__ __forceinline__ bool quad_coop(const StepArgs& a, int ndone) {
 #endif
 }
 
+// The single-done early record's terminal info by a second wave (round 5): the commit
+// wave loads the record, the info wave (kQuadInfoWave) the env's current rows in round
+// 2; at the done path the info wave reduces and stores the info while the commit wave
+// takes the record -- the info's wave reductions off the one-done block's critical path.
+// The commit wave parks the env's post-step scalars + wfix in free table words
+// (dist[24..28]) before the done barrier.  A/B: -DPE_INFO_WAVE=0.
+#ifndef PE_INFO_WAVE
+#define PE_INFO_WAVE 1
+#endif
+constexpr int kQuadInfoWave = 2;  // (4-wave kernels; the slice / position wave)
+constexpr int kInfoParkF = 24;    // floats 24..28 of dist[] (dist[0..R+1] and the one-hot rows at 48.. in use)
+__device__ __forceinline__ bool el_info_hit(int64_t e_info, int64_t e0, const float* smem) {
+  // the block's one done env (the done mask in dist[70..71]) is the info wave's early env
+  const uint64_t dmw = reinterpret_cast<const uint64_t*>(smem)[35];
+  return e_info >= 0 && e_info == e0 + (__ffsll((unsigned long long)dmw) - 1);
+}
+
 // BT: the obs tile holds byte codes (ctab: the LDS code table), see pe_step_quad.
 template <int NW, bool ONEWORD, int KD, bool BT = false>  // one copy per kernel: each inherits its kernel's register budget
 __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, int C, int R, int lane, int wv, int CW,
@@ -640,7 +657,8 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
                                                 const float* ctab = nullptr, const float* stage = nullptr,
                                                 bool stage_info = false, int64_t e_early = -1,
                                                 const PfLoad<ONEWORD ? 1 : kCoopWPR, KD>* early = nullptr,
-                                                const Row4<ONEWORD ? 1 : kCoopWPR>* early_rows = nullptr) {
+                                                const Row4<ONEWORD ? 1 : kCoopWPR>* early_rows = nullptr,
+                                                int64_t e_info = -1) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const StepArgs& a = *reinterpret_cast<const StepArgs*>(ka);
   const Geo& g = a.g;
@@ -657,6 +675,8 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
   const int64_t e = e0 + lane;
   Scal s = unpack(sp);
   constexpr int MAXW = ONEWORD ? 1 : kCoopWPR;
+  // the early record's terminal info is the info wave's (the kernel's kInfoW)
+  constexpr bool kIW = PE_INFO_WAVE && NW == 4 && ONEWORD && !BT && KD <= 2;
   // an obs tile value as a float (BT: expand the code)
   auto tval = [&](const OT* r, int k) -> float {
     if constexpr (BT) return ctab[r[k]];
@@ -697,7 +717,8 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
 #pragma unroll
         for (int j = 0; j < KD; ++j) tv[j] = lane + 64 * j < g.D ? tval(orow, lane + 64 * j) : 0.0f;
         PE_DSTAMP(1);
-        if (a.tinfo) coop_info_store<MAXW>(st, g, *early_rows, sv, a.tinfo + el * PE_NINFO, lane, wf, ltab);
+        // (the terminal info: the info wave's, below, when it loaded the env's rows)
+        if (a.tinfo && !kIW) coop_info_store<MAXW>(st, g, *early_rows, sv, a.tinfo + el * PE_NINFO, lane, wf, ltab);
         PE_DSTAMP(2);
         Row4<MAXW> rw;
         Scal ns;
@@ -777,6 +798,17 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         }
         PE_DSTAMP(5);
       }
+    } else if (kIW && a.tinfo && wv == kQuadInfoWave && el_info_hit(e_info, e0, smem)) {
+      // the terminal info of the early-record env (_get_info, plantos_env.py:317-336) by
+      // the info wave, beside the commit wave's reset: the env's rows came with round 2,
+      // its post-step scalars through LDS (quad_info_park)
+      const float* pk = smem + kInfoParkF;
+      const uint4 spk = make_uint4((uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(pk[0])),
+                                   (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(pk[1])),
+                                   (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(pk[2])),
+                                   (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(pk[3])));
+      const int wf = __builtin_amdgcn_readfirstlane(__float_as_int(pk[4]));
+      coop_info_store<MAXW>(st, g, *early_rows, unpack(spk), a.tinfo + e_info * PE_NINFO, lane, wf, ltab);
     }
     __syncthreads();  // the fresh obs row is in the tile
     __builtin_amdgcn_s_waitcnt(0x0F70);  // see the end of the path below
@@ -839,9 +871,9 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         PfLoad<MAXW, KD> pl;
         if (a.pf.scal && !eh) coop_load_prefetched<MAXW, KD>(a.pf, g, el, pl, lane);
         if (a.tinfo) {
-          if (eh)
+          if (eh && !kIW)
             coop_info_store<MAXW>(st, g, *early_rows, sv, a.tinfo + el * PE_NINFO, lane, kw >> 1, ltab);
-          else
+          else  // (with the info wave the early rows are that wave's, not this one's)
             coop_write_info<MAXW>(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, kw >> 1, ltab);
         }
         Row4<MAXW> rw;
@@ -1341,20 +1373,29 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   constexpr bool kEarlyRec = !BT && ONEWORD && EPB == LS && KDQ <= 2;
   PfLoad<MAXWQ, KDQ> epl;
   Row4<MAXWQ> eir;
-  int64_t e_early = -1;
+  int64_t e_early = -1, e_info = -1;
+  constexpr bool kInfoW = kEarlyRec && PE_INFO_WAVE && NW == 4;
+  static_assert(!kInfoW || (RM + 2 <= kInfoParkF && kInfoParkF + 5 <= kOneHotF), "info park words inside dist[]");
   if constexpr (kEarlyRec) {
     // (the commit wave only, for a block with exactly one: records for up to one
     // predicted env per wave took the desynchronized step 11.16 -> 11.06 us but the
-    // synchronized one 9.42 -> 9.49, profiles/r3g_ab_*.jsonl)
-    if (wv == CW && a.pf.scal && a.autoreset && !st.cur) {
+    // synchronized one 9.42 -> 9.49, profiles/r3g_ab_*.jsonl; round 5: the env's rows
+    // for its terminal info by the info wave)
+    if ((wv == CW || (kInfoW && wv == kQuadInfoWave)) && a.pf.scal && a.autoreset && !st.cur) {
       const uint64_t pmk = __ballot(live && s.step + 1 >= rl.max_steps);
       const uint32_t plo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pmk),
                      phi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pmk >> 32));
       const uint64_t pmu = (uint64_t)plo | ((uint64_t)phi << 32);
       if (__popcll(pmu) == 1) {
-        e_early = e0 + (__ffsll((unsigned long long)pmu) - 1);
-        coop_load_prefetched<MAXWQ, KDQ>(a.pf, g, e_early, epl, lane);
-        eir = coop_info_rows<MAXWQ>(st, g, e_early, lane);
+        const int64_t ep = e0 + (__ffsll((unsigned long long)pmu) - 1);
+        if (wv == CW) {
+          e_early = ep;
+          coop_load_prefetched<MAXWQ, KDQ>(a.pf, g, e_early, epl, lane);
+          if constexpr (!kInfoW) eir = coop_info_rows<MAXWQ>(st, g, e_early, lane);
+        } else {
+          e_info = ep;
+          eir = coop_info_rows<MAXWQ>(st, g, e_info, lane);
+        }
       }
     }
   }
@@ -1529,7 +1570,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // (not asm), so that the done path's first use of it carries none -- otherwise it
   // waits vmcnt(0) there, i.e. for the commit's stores too (in-order counter)
   if constexpr (kEarlyRec) {
-    if (wv == CW) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    if (wv == CW || (kInfoW && wv == kQuadInfoWave)) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   }
   PE_STAMP(2);
   __syncthreads();
@@ -1548,6 +1589,16 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   bool done = false, wfix = false;
   quad_compute<C, R, ONEWORD, NW, BT, RT, false, DV>(a, lrow, lvis, rows, tdist, tpos, tvis, lane, wv, e, live, Cr,
                                                      Rr, m, eo, en, cthr, vp0, s, ret, done, wfix);
+  if constexpr (kInfoW) {  // the early env's post-step scalars for the info wave (read after the done barrier)
+    if (wv == CW && e_early >= 0 && e == e_early) {
+      const uint4 pk = pack(s);
+      smem[kInfoParkF] = __int_as_float((int)pk.x);
+      smem[kInfoParkF + 1] = __int_as_float((int)pk.y);
+      smem[kInfoParkF + 2] = __int_as_float((int)pk.z);
+      smem[kInfoParkF + 3] = __int_as_float((int)pk.w);
+      smem[kInfoParkF + 4] = __int_as_float((int)wfix);
+    }
+  }
   PE_STAMP(4);
   // ---- DummyVecEnv auto-reset (rare): commit wave, after the whole obs row is in LDS
   // any env of the block done (the usual answer: no)?  The commit wave's done mask
@@ -1582,7 +1633,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
     const bool staged = stage_ok && npred == 1 && ndone == 1;  // then the done env is the predicted one
     const uint4 ns = quad_done_path<NW, ONEWORD, (5 * CM + 27 + 63) / 64, BT>(
         kernargs(), tile_off, Cr, Rr, lane, wv, CW, e0, done, pack(s), ret, ndone, wfix, ctab,
-        staged ? stage : nullptr, staged && stage_info, e_early, &epl, &eir);
+        staged ? stage : nullptr, staged && stage_info, e_early, &epl, &eir, e_info);
     s = unpack(ns);
   }
   // the obs tile goes out through the waves other than the commit wave: its state
