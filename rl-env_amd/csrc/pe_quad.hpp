@@ -137,51 +137,52 @@ __device__ __forceinline__ void quad_rays(const uint64_t* lrow, int lane, int kc
 
 // Runtime-(C, R) sector rays: the ray march of pe_step_quad<0, 0, ...> (the table-
 // driven sector kernel of geometries with no compile-time specialization, C <= 64,
-// 2 <= R <= 14).  Wave wv's rays [wv*C/NW, (wv+1)*C/NW); the probe offsets are
-// wave-uniform (the packed (dx & 0xFF | dy << 8) table st.ldxy, R rounded up to 8
-// per ray and zero-padded, copied into LDS by the kernel: read from global memory it
-// was a vector load per 8-probe chunk that each ray waited out): 8 probes per 16-B LDS
-// read at a wave-uniform address, unrolled, so that a ray's window reads are in flight
-// together instead of one round trip per probe; a probe is one LDS read of the window row at the lane's row
-// offset, a shift and the same 2-bit packing as quad_rays (first hit by one
-// find-first-set; plantos_env.py:260-292).
+// 2 <= R <= 14).  Wave wv's rays [wv*C/NW, (wv+1)*C/NW); the probes are wave-uniform
+// u32 entries of an LDS table (pe_create, round 5): the probe's LDS byte offset from the
+// lane's rover row (dx * 64 envs * 8 B, int16) | its bit shift in the funnel-shifted row
+// word (2(dy+R)) << 16 -- 4 probes per 16-B LDS read at a wave-uniform address, unrolled
+// by 8; a probe is one address add, one LDS read, one shift add, the 64-bit shift and the
+// 2-bit pack (plantos_env.py:260-292; first hit by one find-first-set).  The watered
+// rover cell (code 3 -> 2) is fixed per ray, not per probe: it is the ray's first probe
+// (r = 1 at (0, 0), the only radius where int(r cos) = int(r sin) = 0), a hit either way,
+// so only that ray's entity changes (round 4's per-probe mask: ~10 VALU per probe).
 template <typename OT>
-__device__ __forceinline__ void quad_rays_rt(const uint64_t* lrow, const int16_t* ldxy, int i0, int i1, int R,
+__device__ __forceinline__ void quad_rays_rt(const uint64_t* lrow, const uint32_t* ltab, int i0, int i1, int R,
                                              int lane, int kc, int sh, bool watered, OT* row, const float* tdist) {
   const int RP = (R + 7) & ~7;
   const uint32_t kNZ = 0x55555555u & ((1u << (2 * R)) - 1u);  // R <= 14
   const float4* tone = reinterpret_cast<const float4*>(tdist + kOneHotF);
-  const uint64_t wclr = ~((uint64_t)(watered ? 1u : 0u) << (sh + 2 * R));  // the rover's cell: 3 -> 2 (watered)
-  // (tried: the lane's row base and shift folded in once, the watered fix-up per ray
-  // instead of per probe -- 5 VALU per probe instead of ~11, measured slower: 40x40/C48/R8
-  // 31.10 -> 31.40 us, profiles/r4af/)
+  const char* base = reinterpret_cast<const char*>(lrow + kc * kQuadEnvs + lane);  // the lane's rover row
+  const uint32_t origin = (uint32_t)(2 * R) << 16;  // the entry of probe (0, 0)
   for (int i = i0; i < i1; ++i) {
-    const uint4* o4 = reinterpret_cast<const uint4*>(ldxy + i * RP);  // (16-B aligned: RP is a multiple of 8)
+    const uint4* o4 = reinterpret_cast<const uint4*>(ltab + i * RP);  // (16-B aligned: RP is a multiple of 8)
     uint32_t pk = 0u;
     auto probe = [&](uint32_t v, int r) {
-      const int dx = (int)(int8_t)(v & 0xFFu), dy = (int)(int8_t)((v >> 8) & 0xFFu);
-      uint64_t w = lrow[(kc + dx) * kQuadEnvs + lane];
-      w &= dx == 0 ? wclr : ~0ull;
-      pk |= (uint32_t)((w >> (sh + 2 * (dy + R))) & 3u) << (2 * r);  // (r < R <= 14)
+      const uint64_t w = *reinterpret_cast<const uint64_t*>(base + (int)(int16_t)(v & 0xFFFFu));
+      pk |= (uint32_t)((w >> (sh + (int)(v >> 16))) & 3u) << (2 * r);  // (r < R <= 14)
     };
+    uint32_t first = 0u;
     int r0 = 0;
     for (; r0 + 8 <= R; r0 += 8) {  // whole chunks: 8 probes unrolled, their LDS reads in flight together
-      const uint4 q = o4[r0 >> 3];
-      const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+      const uint4 qa = o4[r0 >> 2], qb = o4[(r0 >> 2) + 1];
+      const uint32_t qw[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+      if (r0 == 0) first = qa.x;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) probe(qw[j >> 1] >> (16 * (j & 1)), r0 + j);
+      for (int j = 0; j < 8; ++j) probe(qw[j], r0 + j);
     }
-    if (r0 < R) {  // the last R % 8 probes: one scalar load, then a loop (padded probes not marched:
-                   // R = 9 marching all 16 was 10 % slower than the per-probe loads, profiles/r4m)
-      const uint4 q = o4[r0 >> 3];
+    if (r0 < R) {  // the last R % 8 probes (padded probes not marched: profiles/r4m)
+      const uint4 qa = o4[r0 >> 2], qb = o4[(r0 >> 2) + 1];
+      if (r0 == 0) first = qa.x;
       for (int j = 0; j < R - r0; ++j) {
-        const uint32_t qj = j < 2 ? q.x : (j < 4 ? q.y : (j < 6 ? q.z : q.w));
-        probe(qj >> (16 * (j & 1)), r0 + j);
+        const uint32_t qj = j < 4 ? (j < 2 ? (j == 0 ? qa.x : qa.y) : (j == 2 ? qa.z : qa.w))
+                                  : (j < 6 ? (j == 4 ? qb.x : qb.y) : (j == 6 ? qb.z : qb.w));
+        probe(qj, r0 + j);
       }
     }
     const uint32_t nz = ((pk | (pk >> 1)) & kNZ) | (1u << (2 * R));
     const int f = __builtin_ctz(nz);        // 2r of the first hit, 2R if none
-    const int ent = (int)((pk >> f) & 3u);  // its code (EMPTY if none)
+    int ent = (int)((pk >> f) & 3u);        // its code (EMPTY if none)
+    if (watered && f == 0 && first == origin) ent &= 2;  // the watered rover cell: THIRSTY -> HYD
     if constexpr (std::is_same<OT, float>::value) {
       const float dv = tdist[(f >> 1) + 1];
       const float4 ov = tone[ent];

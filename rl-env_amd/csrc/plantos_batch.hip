@@ -613,7 +613,7 @@ __host__ __device__ constexpr int quad_rtab_off(int C, bool bt) {
 }
 // the runtime sector kernel's probe table in LDS (floats; C rays x R rounded up to 8
 // int16 entries), placed after the tile (+ code table) and before the staging region
-__host__ __device__ constexpr int quad_rtab_floats(int C, int R) { return ((C * ((R + 7) & ~7) * 2 + 15) / 16) * 4; }
+__host__ __device__ constexpr int quad_rtab_floats(int C, int R) { return C * ((R + 7) & ~7); }  // u32 entries
 
 // ---- pe_step_quad's auto-reset slow path (a block with a done env), out of line:
 // kept in separate functions so that their register demand (map generation, the
@@ -1089,7 +1089,7 @@ __device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* 
     const int sh = 2 * (yp - m.yb);
     const int vs = 4 * (yp - m.ybv);
     if constexpr (RT) {
-      const int16_t* ltab = reinterpret_cast<const int16_t*>(reinterpret_cast<const float*>(rows) + quad_rtab_off(Cr, BT));
+      const uint32_t* ltab = reinterpret_cast<const uint32_t*>(reinterpret_cast<const float*>(rows) + quad_rtab_off(Cr, BT));
       quad_rays_rt<OT>(lrow, ltab, wv * Cr / NW, (wv + 1) * Cr / NW, Rr, lane, kc, sh, watered, row, tdist);
     } else {
       sector_rays<C, R, NW>(wv, lrow, lane, kc, sh, watered, row, tdist);
@@ -1317,7 +1317,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
                        // loop, each 8-probe chunk was a vector load waited out with vmcnt(0)
     const uint4* src = reinterpret_cast<const uint4*>(st.ldxy);
     uint4* dst = reinterpret_cast<uint4*>(smem + tail_off);
-    for (int k = threadIdx.x; k < Cr * ((Rr + 7) & ~7) / 8; k += blockDim.x) dst[k] = src[k];
+    for (int k = threadIdx.x; k < Cr * ((Rr + 7) & ~7) / 4; k += blockDim.x) dst[k] = src[k];  // (u32 entries)
   }
   Scal s = unpack(sw);
 #ifdef PE_STAMPS
@@ -3242,7 +3242,8 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   const size_t o_ldx = carve(nl), o_ldy = carve(nl);
   const int RP = (R + 7) & ~7;
   const bool wave_aln = h->variant == V_GENERIC && wave_aln_ok(G, R, g.WPR);  // pe_step_wave<., true>
-  const size_t o_ldxy = carve(wave_aln ? ((size_t)C * RP * 3 + 15) & ~(size_t)15 : (size_t)C * RP * 2);
+  const bool rt_tab = h->variant == V_QUAD_RT_1W || h->variant == V_QUAD_RT;  // u32 probe entries (quad_rays_rt)
+  const size_t o_ldxy = carve(wave_aln ? ((size_t)C * RP * 3 + 15) & ~(size_t)15 : (size_t)C * RP * (rt_tab ? 4 : 2));
   const size_t o_err = carve(sizeof(uint32_t));
   const size_t o_scal = carve(n * sizeof(uint4));
   const size_t o_ret = carve(n * sizeof(double));
@@ -3327,6 +3328,14 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
       aln[2 * ldxy.size() + k] = (uint8_t)((en >> 11) & 31u);
     }
     e5 = hipMemcpy(base + o_ldxy, aln.data(), aln.size(), hipMemcpyHostToDevice);
+  } else if (rt_tab) {  // the runtime sector kernel's entries (pe_quad.hpp quad_rays_rt): the probe's LDS
+                        // byte offset from the rover row (dx rows of 64 envs x 8 B) | its bit shift 2(dy+R) << 16
+    std::vector<uint32_t> rt((size_t)C * RP, 0u);
+    for (int i = 0; i < C; ++i)
+      for (int r = 0; r < R; ++r)
+        rt[(size_t)i * RP + r] = (uint32_t)(uint16_t)(int16_t)(ldx[i * R + r] * kQuadEnvs * 8) |
+                                 ((uint32_t)(2 * (ldy[i * R + r] + R)) << 16);
+    e5 = hipMemcpy(base + o_ldxy, rt.data(), rt.size() * 4, hipMemcpyHostToDevice);
   } else {
     e5 = hipMemcpy(base + o_ldxy, ldxy.data(), ldxy.size() * 2, hipMemcpyHostToDevice);
   }
