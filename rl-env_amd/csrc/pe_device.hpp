@@ -191,14 +191,26 @@ struct Scal {
 // atomic store is a plain store with sc1 (MI355X: the line goes on to the
 // Infinity Cache / HBM at once instead of staying dirty in the XCD's L2), so the
 // kernel-end L2 writeback has nothing of it left to flush at the launch boundary.
+#ifndef PE_SCAL_STORE16
+#define PE_SCAL_STORE16 1  // 16-B packed-scalar stores (headline 9.54 -> 9.28 us, desync 10.57 -> 10.40; A/B: 0)
+#endif
 template <typename T>
 __device__ __forceinline__ void st_wt(T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void st_wt(uint4* p, uint4 v) {
+#if PE_SCAL_STORE16
+  // one 16-B write-through store (the packed scalars of consecutive lanes are contiguous:
+  // whole lines per wave-instruction) -- two 8-B atomic stores left every line half
+  // written per instruction
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const v4u d = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(d) : "memory");
+#else
   uint64_t* q = reinterpret_cast<uint64_t*>(p);
   st_wt(q, (uint64_t)v.x | ((uint64_t)v.y << 32));
   st_wt(q + 1, (uint64_t)v.z | ((uint64_t)v.w << 32));
+#endif
 }
 
 __device__ __forceinline__ Scal unpack(uint4 w) {

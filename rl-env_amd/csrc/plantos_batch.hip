@@ -1165,8 +1165,13 @@ __device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* 
           // nibbles): one byte store, no read of the word from memory
           const int p = m.ny + 2, b = p >> 1;
           const uint32_t wnew = (lvis[(3 + m.dxm) * LS + lane] & ~(0xFu << (4 * (p - m.ybv)))) | (nib << (4 * (p - m.ybv)));
+#if defined(PE_PROBE_VISIDLE)  // (timing / traffic probe, wrong results: the byte into the idle slot)
+          st_wt(reinterpret_cast<uint8_t*>(vis_env(st, g, e, s.episode ^ 1u) + (int64_t)m.nx * g.NW) + b,
+                (uint8_t)(wnew >> (4 * (2 * b - m.ybv))));
+#else
           st_wt(reinterpret_cast<uint8_t*>(vis_env(st, g, e, s.episode) + (int64_t)m.nx * g.NW) + b,
                 (uint8_t)(wnew >> (4 * (2 * b - m.ybv))));
+#endif
           if constexpr (DV)
             np = vx_pending(m.cell_n, n);
           else
@@ -1193,18 +1198,22 @@ __device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* 
         }
       }
       ret += rew;
+#if !defined(PE_PROBE_NOOUT)
       st_wt(a.reward + e, (float)rew);
       st_wt(a.term + e, (uint8_t)term);
       st_wt(a.trunc + e, (uint8_t)trunc);
+#endif
       if (done) {  // Monitor's episode return / length of the ended episode
         if (a.ep_ret_out) st_wt(a.ep_ret_out + e, ret);
         if (a.ep_len_out) st_wt(a.ep_len_out + e, (int32_t)s.step);
       }
       // an env about to be auto-reset: its reset path stores the new episode's scalars
+#if !defined(PE_PROBE_NOSCAL)
       if (!(done && a.autoreset && !st.cur)) {
         st_wt(st.ep_ret + e, ret);
         st_wt(st.scal + e, pack(s));
       }
+#endif
       if constexpr (DV) {
         if (vp0 | np) st_wt(st.vpend + e, np);
       }
