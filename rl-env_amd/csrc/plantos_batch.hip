@@ -2577,7 +2577,13 @@ __global__ void pe_synth_kernel(int n, uint64_t seed, uint32_t env_off, uint32_t
 // f32 | terminated | truncated, block b at src + b * stride) -> contiguous f32 obs
 // (+ the other outputs).  Grid: (x: 16-B output chunks, y: block); one u32 of 4 codes
 // per thread through the LDS code table, one 16-B store.
-constexpr int kExpandPer = 4;  // 4-code groups per thread (the table build amortized over 4 of them)
+#ifndef PE_EXPAND_PER
+#define PE_EXPAND_PER 4
+#endif
+#ifndef PE_EXPAND_SC1
+#define PE_EXPAND_SC1 1  // write-through expanded obs (expansion 7.85 -> 5.93 us, gather leg 20.45 -> 19.4; A/B: 0)
+#endif
+constexpr int kExpandPer = PE_EXPAND_PER;  // 4-code groups per thread (the table build amortized over them)
 __global__ __launch_bounds__(256) void pe_expand_codes_kernel(const Tables* tab, int R, int G, int D, int rows,
                                                               const uint8_t* src, int64_t stride, float* obs,
                                                               float* rew, uint8_t* te, uint8_t* tr) {
@@ -2603,12 +2609,17 @@ __global__ __launch_bounds__(256) void pe_expand_codes_kernel(const Tables* tab,
     for (int j = 0; j < kExpandPer; ++j) {
       const int64_t k = g0 + 256 * j;
       if (4 * k < nc) {
-        float4 v;
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        v4f v;
         v.x = ctab[c[j] & 255u];
         v.y = ctab[(c[j] >> 8) & 255u];
         v.z = ctab[(c[j] >> 16) & 255u];
         v.w = ctab[c[j] >> 24];
-        *reinterpret_cast<float4*>(ob + 4 * k) = v;
+#if PE_EXPAND_SC1  // the expanded obs stream write-through, as the step kernels' tile stores
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(ob + 4 * k), "v"(v) : "memory");
+#else
+        *reinterpret_cast<v4f*>(ob + 4 * k) = v;
+#endif
       }
     }
   } else {
