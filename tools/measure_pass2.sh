@@ -1,22 +1,10 @@
 #!/usr/bin/env bash
-# The measurement pass of the product library (tools/gpu_session.sh steps): the GPU suite,
-# smoke, bench lines of every geometry, rocprof kernel stats and FETCH / WRITE PMC passes.
-# Copy it into profiles/ with tools/summarize_pass.sh TAG.
-#   usage: bash tools/measure_pass.sh TAG
+# The measurement pass's profiling half (tools/measure_pass.sh, split in two gpurun calls):
+# rocprof kernel stats of every geometry and the FETCH / WRITE PMC passes.
+#   usage: bash tools/measure_pass2.sh TAG
 set -euo pipefail
-OUT=gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
 T=$1
-bash tools/gpu_session.sh $T tests
-tail -n 1 $OUT/tests_$T.log
-bash tools/gpu_session.sh $T smoke bench benchx:drv:--steps_20_--warmup_5 bench64 \
-  benchx:n4096:--envs_4096_--steps_20000_--warmup_1000_--desync-steps_20000_--cpu-seconds_5 \
-  benchx:g25:--grid_25_--steps_20000_--warmup_1000_--cpu-seconds_5 \
-  benchx:g21:--grid_21_--rays_10_--range_2_--plants_8_--obstacles_50_--steps_20000_--warmup_1000_--cpu-seconds_5 \
-  benchx:g15:--grid_15_--rays_16_--range_4_--plants_6_--obstacles_8_--steps_20000_--warmup_1000_--cpu-seconds_5 \
-  benchx:g32:--grid_32_--rays_24_--range_9_--plants_20_--obstacles_30_--steps_4000_--warmup_200_--desync-steps_4000_--cpu-seconds_5 \
-  benchx:g64r32:--grid_64_--rays_64_--range_32_--steps_2000_--warmup_100_--desync-steps_2000_--cpu-seconds_5 \
-  benchx:g40c48:--grid_40_--rays_48_--range_8_--steps_2000_--warmup_100_--desync-steps_2000_--cpu-seconds_5 \
-  stats statsd stats64 \
+bash tools/gpu_session.sh $T stats statsd stats64 \
   statsx:n4096:--envs_4096_--steps_4096_--warmup_200_--desync-steps_0_--gather-steps_0_--no-cpu-baseline \
   statsx:g25:--grid_25_--steps_4096_--warmup_200_--desync-steps_0_--gather-steps_0_--no-cpu-baseline \
   statsx:g64r32:--grid_64_--rays_64_--range_32_--steps_1000_--warmup_50_--desync-steps_0_--gather-steps_0_--no-cpu-baseline \
@@ -29,4 +17,4 @@ bash tools/gpu_session.sh $T smoke bench benchx:drv:--steps_20_--warmup_5 bench6
   pmcx:g40c48:FETCH_SIZE:--grid_40_--rays_48_--range_8 pmcx:g40c48:WRITE_SIZE:--grid_40_--rays_48_--range_8 \
   pmcx:g32:FETCH_SIZE:--grid_32_--rays_24_--range_9_--plants_20_--obstacles_30 \
   pmcx:g32:WRITE_SIZE:--grid_32_--rays_24_--range_9_--plants_20_--obstacles_30
-echo pass done
+echo pass2 done

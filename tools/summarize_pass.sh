@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Copy a measurement pass (tools/measure_pass.sh TAG) from gpurun_out/ into
+# Copy a measurement pass (tools/measure_pass1.sh TAG, then tools/measure_pass2.sh TAG) from gpurun_out/ into
 # profiles/ under the names the docs cite, and write the PMC summaries (tools/pmc_summary.py).
 #   usage: bash tools/summarize_pass.sh TAG
 set -euo pipefail
