@@ -107,7 +107,9 @@ typedef struct pe_config {
                                    can hold a byte-coded tile: C = 16 / R = 6 with G <= 20,
                                    C = 64 / R = 6, and every geometry of the runtime-(C, R)
                                    sector kernel (4 <= C <= 64, 2 <= R <= 14, no compile-
-                                   time kernel); pe_create fails with PE_ERR_ARG elsewhere.
+                                   time kernel), and the far sector kernel's C = 64 / R = 32
+                                   with 96 < G + 2R <= 128; pe_create fails with PE_ERR_ARG
+                                   elsewhere.
                                    pe_step still writes f32 obs on such a handle.
                                    0 (default): off                                     */
     int32_t reserved[3];
