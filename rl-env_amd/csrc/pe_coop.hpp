@@ -592,15 +592,19 @@ __device__ inline void coop_write_info(const State& st, const Geo& g, int64_t e,
 // its rows to rw and its fresh obs row (D <= 64 * KD floats) to out.  Short rows
 // come in with the record (one round trip); longer ones after the check
 // (registers).
+// OT: the record's obs row type -- floats, or (a byte-coded handle) D byte codes,
+// loaded early as 4-code words (lane k: codes 4k..4k+3; the row is 16-B aligned and
+// padded to ostride, so the last word stays inside it) and written to a byte-coded
+// tile row at the take.
 template <int MAXW, int KD>
 struct PfLoad {
   static constexpr bool kEarly = KD <= 2;
   uint4 ps;
   Row4<MAXW> rw;
-  float ov[kEarly ? KD : 1];
+  float ov[kEarly ? KD : 1];  // (codes: 4-code words, bit-cast)
 };
 
-template <int MAXW, int KD>
+template <int MAXW, int KD, typename OT = float>
 __device__ __forceinline__ void coop_load_prefetched(const Prefetch& pf, const Geo& g, int64_t e,
                                                      PfLoad<MAXW, KD>& L, int lane) {
   L.ps = pf.scal[e];
@@ -612,15 +616,22 @@ __device__ __forceinline__ void coop_load_prefetched(const Prefetch& pf, const G
       if (MAXW == 1 || w < g.WPR) L.rw.set(w, src[w]);
   }
   if constexpr (PfLoad<MAXW, KD>::kEarly) {
-    const float* osrc = pf_obs_row(pf, e);
+    if constexpr (sizeof(OT) == 1) {
+      const uint32_t* osrc = reinterpret_cast<const uint32_t*>(pf_obs_row(pf, e));
+      const int nw = (g.D + 3) >> 2;
 #pragma unroll
-    for (int j = 0; j < KD; ++j) L.ov[j] = lane + 64 * j < g.D ? osrc[lane + 64 * j] : 0.0f;
+      for (int j = 0; j < KD; ++j) L.ov[j] = lane + 64 * j < nw ? __uint_as_float(osrc[lane + 64 * j]) : 0.0f;
+    } else {
+      const float* osrc = pf_obs_row(pf, e);
+#pragma unroll
+      for (int j = 0; j < KD; ++j) L.ov[j] = lane + 64 * j < g.D ? osrc[lane + 64 * j] : 0.0f;
+    }
   }
 }
 
-template <int MAXW, int KD>
+template <int MAXW, int KD, typename OT = float>
 __device__ __forceinline__ bool coop_take_prefetched(const Prefetch& pf, const Geo& g, int64_t e, uint32_t episode,
-                                                     const PfLoad<MAXW, KD>& L, Row4<MAXW>& rw, Scal& s, float* out,
+                                                     const PfLoad<MAXW, KD>& L, Row4<MAXW>& rw, Scal& s, OT* out,
                                                      int lane) {
   const uint32_t key = (uint32_t)__builtin_amdgcn_readfirstlane((int)L.ps.w);
   if (key != episode + 1u) return false;
@@ -628,13 +639,23 @@ __device__ __forceinline__ bool coop_take_prefetched(const Prefetch& pf, const G
                         (uint32_t)__builtin_amdgcn_readfirstlane((int)L.ps.y),
                         (uint32_t)__builtin_amdgcn_readfirstlane((int)L.ps.z), key));
   rw = L.rw;
-  if (!out) return true;  // a byte-coded record: the caller copies it (coop_copy_record_codes)
   if constexpr (PfLoad<MAXW, KD>::kEarly) {
+    if constexpr (sizeof(OT) == 1) {
 #pragma unroll
-    for (int j = 0; j < KD; ++j)
-      if (lane + 64 * j < g.D) out[lane + 64 * j] = L.ov[j];
+      for (int j = 0; j < KD; ++j) {
+        const int k = 4 * (lane + 64 * j);
+        const uint32_t w = __float_as_uint(L.ov[j]);
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          if (k + b < g.D) out[k + b] = (OT)(w >> (8 * b));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < KD; ++j)
+        if (lane + 64 * j < g.D) out[lane + 64 * j] = L.ov[j];
+    }
   } else {
-    const float* osrc = pf_obs_row(pf, e);
+    const OT* osrc = reinterpret_cast<const OT*>(pf_obs_row(pf, e));
     for (int k = lane; k < g.D; k += 64) out[k] = osrc[k];
   }
   return true;
@@ -788,14 +809,6 @@ __device__ inline void coop_fresh_obs(const Geo& g, const Row4<MAXW>& rw, const 
   } else if (lane < 27) {
     out[5 * C + lane - 25] = w.pos(lane == 25 ? s.x : s.y);  // :294-296
   }
-}
-
-// The prefetched record's obs row as codes (a byte-coded handle: pf.obs holds D
-// bytes per env) copied into a byte-coded tile row, once the record is taken.
-__device__ __forceinline__ void coop_copy_record_codes(const Prefetch& pf, const Geo& g, int64_t e, uint8_t* out,
-                                                       int lane) {
-  const uint8_t* src = reinterpret_cast<const uint8_t*>(pf_obs_row(pf, e));
-  for (int k = lane; k < g.D; k += 64) out[k] = src[k];
 }
 
 // ---- A block's single done env: its prefetched record staged into LDS by LDS-DMA

@@ -536,6 +536,9 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
 #ifndef PE_BT_DV
 #define PE_BT_DV 1  // the byte-coded C16R6 kernel defers its overflow writes as the f32 one (A/B: 0)
 #endif
+#ifndef PE_BT_EARLY
+#define PE_BT_EARLY 1  // the byte-coded one-word kernel loads a predicted single truncation's record early (A/B: 0)
+#endif
 #ifndef PE_BT_STAGE_MIN_C
 #define PE_BT_STAGE_MIN_C 64  // byte-coded kernels stage the predicted record by LDS-DMA from this C on (A/B: 0)
 #endif
@@ -676,7 +679,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
   Scal s = unpack(sp);
   constexpr int MAXW = ONEWORD ? 1 : kCoopWPR;
   // the early record's terminal info is the info wave's (the kernel's kInfoW)
-  constexpr bool kIW = PE_INFO_WAVE && NW == 4 && ONEWORD && !BT && KD <= 2;
+  constexpr bool kIW = PE_INFO_WAVE && NW == 4 && ONEWORD && KD <= 2;
   // an obs tile value as a float (BT: expand the code)
   auto tval = [&](const OT* r, int k) -> float {
     if constexpr (BT) return ctab[r[k]];
@@ -684,13 +687,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
   };
   // a prefetched record's fresh obs row into tile row `o` once taken (BT: codes)
   auto take = [&](int64_t el, uint32_t episode, const PfLoad<MAXW, KD>& pl, Row4<MAXW>& rw, Scal& ns, OT* o) -> bool {
-    if constexpr (BT) {
-      if (!coop_take_prefetched<MAXW, KD>(a.pf, g, el, episode, pl, rw, ns, nullptr, lane)) return false;
-      coop_copy_record_codes(a.pf, g, el, o, lane);
-      return true;
-    } else {
-      return coop_take_prefetched<MAXW, KD>(a.pf, g, el, episode, pl, rw, ns, o, lane);
-    }
+    return coop_take_prefetched<MAXW, KD, OT>(a.pf, g, el, episode, pl, rw, ns, o, lane);
   };
   if (ndone == 1 && quad_coop(a, ndone)) {
     // One done env (the usual case with desynchronized episodes): the commit wave,
@@ -702,7 +699,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
       const int64_t el = e0 + l;
       OT* orow = rows + l * g.D;
       // early: the kernel loaded this env's record and rows behind the compute phase
-      const bool early_hit = !BT && KD <= 2 && early != nullptr && el == e_early;
+      const bool early_hit = KD <= 2 && early != nullptr && el == e_early;
       if (early_hit) {
         // the record and the env's rows were loaded behind the compute phase (the
         // kernel's early record): every wait here is for loads issued ~1 us ago.
@@ -748,7 +745,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
       } else {
         // the record: staged into LDS before the done barrier (stage), or loaded now
         PfLoad<MAXW, KD> pl;
-        if (a.pf.scal && !stage) coop_load_prefetched<MAXW, KD>(a.pf, g, el, pl, lane);  // in flight from here on
+        if (a.pf.scal && !stage) coop_load_prefetched<MAXW, KD, OT>(a.pf, g, el, pl, lane);  // in flight from here on
         bool keep = false;
         if (done && st.cur) keep = curriculum_on_reset(st.cur, e, rl);  // A2C_training.py:56-95
         const bool kp = __builtin_amdgcn_readlane((int)keep, l) != 0;
@@ -867,9 +864,9 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         const Scal sv = unpack(sl);
         // the prefetched record's loads go out first, the terminal info's after them --
         // or both came with round 2 (the kernel's early record of this wave's env)
-        const bool eh = !BT && KD <= 2 && early != nullptr && el == e_early;
+        const bool eh = KD <= 2 && early != nullptr && el == e_early;
         PfLoad<MAXW, KD> pl;
-        if (a.pf.scal && !eh) coop_load_prefetched<MAXW, KD>(a.pf, g, el, pl, lane);
+        if (a.pf.scal && !eh) coop_load_prefetched<MAXW, KD, OT>(a.pf, g, el, pl, lane);
         if (a.tinfo) {
           if (eh && !kIW)
             coop_info_store<MAXW>(st, g, *early_rows, sv, a.tinfo + el * PE_NINFO, lane, kw >> 1, ltab);
@@ -1366,7 +1363,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   };
   quad_move_cells<ONEWORD>(m, s, g.G);
 
-  // Early record (f32-tile one-word kernels): a block whose ONLY env to truncate this
+  // Early record (one-word 64-env kernels): a block whose ONLY env to truncate this
   // step is known from its step count (:177; ~6 % of the blocks of a desynchronized
   // batch each step) has the commit wave load that env's prefetched record and its
   // grid rows (the terminal info) right before round 2's loads -- they land with them,
@@ -1379,7 +1376,9 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // (one-word 64-env kernels only: the multi-word kernel is at its 128-VGPR cap and
   // spilled with it -- 25x25 desynchronized 14.0 -> 14.6 us -- and the 16-env shape of
   // small batches lost 2-5 % synchronized; profiles/r3c_ab_early_*.jsonl)
-  constexpr bool kEarlyRec = !BT && ONEWORD && EPB == LS && KDQ <= 2;
+  // (round 5: the byte-coded one-word kernel too -- config 5's codes step; the record's
+  // codes come in as 4-code words; A/B: -DPE_BT_EARLY=0)
+  constexpr bool kEarlyRec = (!BT || PE_BT_EARLY) && ONEWORD && EPB == LS && KDQ <= 2;
   PfLoad<MAXWQ, KDQ> epl;
   Row4<MAXWQ> eir;
   int64_t e_early = -1, e_info = -1;
@@ -1399,7 +1398,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
         const int64_t ep = e0 + (__ffsll((unsigned long long)pmu) - 1);
         if (wv == CW) {
           e_early = ep;
-          coop_load_prefetched<MAXWQ, KDQ>(a.pf, g, e_early, epl, lane);
+          coop_load_prefetched<MAXWQ, KDQ, OT>(a.pf, g, e_early, epl, lane);
           if constexpr (!kInfoW) eir = coop_info_rows<MAXWQ>(st, g, e_early, lane);
         } else {
           e_info = ep;

@@ -83,13 +83,27 @@ def test_desync_autoreset_parity(name, n, steps, spread, coop_max, every, reseed
         _desync_run(name, n, steps, spread, coop_max, every, reseed_at, reset_at)
 
 
-def _desync_run(name, n, steps, spread, coop_max, every, reseed_at, reset_at):
+@pytest.mark.parametrize("name,n,steps,spread,coop_max", [
+    ("g20", 2048, 160, 150, None),  # one-done blocks: the early record (4-code words) + the info wave
+    ("g20", 1024, 80, 60, "64"),    # several done envs per block, cooperative, code records
+    ("g20", 256, 12, 1, None),      # every env at once: lane-per-env resets, fresh codes from HBM
+    ("g64", 192, 50, 40, None),     # 64x64: the LDS-DMA staged record
+])
+def test_desync_autoreset_parity_codes(name, n, steps, spread, coop_max):
+    """The byte-coded step (pe_step_codes, config 5's codes gather) through the same
+    desynchronized auto-reset paths: expanded obs, terminal obs / info / return /
+    length and the final state equal the oracle's."""
+    _desync_run(name, n, steps, spread, coop_max, None, None, None, codes=True)
+
+
+def _desync_run(name, n, steps, spread, coop_max, every, reseed_at, reset_at, codes=False):
     from plantos_amd import PlantOSBatch
     G, P, Ob, R, C = cfg = CFG[name]
     seed = aseed = 31
     b = PlantOSBatch(n, grid_size=G, num_plants=P, num_obstacles=Ob, lidar_range=R, lidar_channels=C, seed=seed,
                      device="cuda:0", coop_max_done=None if coop_max is None else int(coop_max),
-                     prefetch_every=None if every is None else int(every))
+                     prefetch_every=None if every is None else int(every), obs_codes=codes)
+    f_obs = torch.empty((n, b.obs_dim), dtype=torch.float32, device="cuda:0") if codes else None
     ov = OracleVec(cfg, np.arange(n), seed)
     # desynchronize: env e starts at step 1000 - 1 - k(e), k in [0, spread)
     rng = np.random.default_rng(5)
@@ -119,6 +133,8 @@ def _desync_run(name, n, steps, spread, coop_max, every, reseed_at, reset_at):
         b.synth_actions(aseed, t, out=act)
         a_np = np_(act)
         obs, rew, te, tr = b.step(act)
+        if codes:  # the step wrote byte codes: expand them (pe_expand_obs_codes)
+            obs = b.expand_codes(b.io, 1, f_obs)[0]
         # oracle: step, pre-reset info of the done envs, then the resets (OracleVec.step)
         o_obs, o_rew, o_te, o_tr = ov.b.step(a_np)
         done = o_te | o_tr
