@@ -620,7 +620,11 @@ __device__ __forceinline__ void coop_load_prefetched(const Prefetch& pf, const G
       const uint32_t* osrc = reinterpret_cast<const uint32_t*>(pf_obs_row(pf, e));
       const int nw = (g.D + 3) >> 2;
 #pragma unroll
-      for (int j = 0; j < KD; ++j) L.ov[j] = lane + 64 * j < nw ? __uint_as_float(osrc[lane + 64 * j]) : 0.0f;
+      for (int j = 0; j < KD; ++j) {  // (unconditional, clamped: a select on the loaded word was waited out
+                                      // at once; the take writes only the codes k < D)
+        const int kk = lane + 64 * j;
+        L.ov[j] = __uint_as_float(osrc[kk < nw ? kk : nw - 1]);
+      }
     } else {
       const float* osrc = pf_obs_row(pf, e);
 #pragma unroll
@@ -750,7 +754,18 @@ struct ObsW<uint8_t> {
   __device__ __forceinline__ uint8_t pos(int x) const { return (uint8_t)(kCodePos + x); }
 };
 
-// The float of code c (one entry per thread when building the LDS code table).
+// The code table entry c in two halves for a kernel's first round: obs_code_loads issues
+// every candidate load unconditionally (with the round's other loads: a load inside the
+// branches of a per-code `if` chain was waited out at once -- three dependent round trips in
+// the byte-coded kernels' first round, ~1.2 us, profiles/r5s/), obs_code_pick selects.
+struct CodeLd {
+  float d, v, p;
+};
+__device__ __forceinline__ CodeLd obs_code_loads(const Tables* tab, int R, int G, int c) {
+  const int px = c - kCodePos;
+  return CodeLd{tab->dist[c <= R ? c : 0], tab->vis[(c - kCodeVis) & 15], tab->pos[px >= 0 && px < G ? px : 0]};
+}
+// The float of code c as one call (the far and C = 64 kernels: after their first round's wait).
 __device__ __forceinline__ float obs_code_value(const Tables* tab, int R, int G, int c) {
   if (c <= R) return tab->dist[c];
   if (c == R + 1) return 1.0f;
@@ -758,6 +773,13 @@ __device__ __forceinline__ float obs_code_value(const Tables* tab, int R, int G,
   if (c >= kCodePos && c < kCodePos + G) return tab->pos[c - kCodePos];
   return 0.0f;
 }
+__device__ __forceinline__ float obs_code_pick(const CodeLd& l, int R, int G, int c) {
+  return c <= R ? l.d
+                : (c == R + 1 ? 1.0f
+                              : ((c >= kCodeVis && c < kCodeVis + 16) ? l.v
+                                                                      : ((c >= kCodePos && c < kCodePos + G) ? l.p : 0.0f)));
+}
+
 
 // build_obs_fresh by one wave from the rows in the lanes' registers: lane i
 // marches ray i (plantos_env.py:260-292), lanes 0..26 the position and the 5x5

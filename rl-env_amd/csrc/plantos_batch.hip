@@ -1311,13 +1311,22 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
       qg1[j] = lgq[q < nq ? q : nq - 1];
     }
   }
+  // (BT: the code table's candidate loads go out with round 1, see obs_code_loads -- codes
+  // step 9.58 -> 9.25 us, 40x40/C48 28.84 -> 28.48; not at C = 64, whose synchronized step
+  // measured 23.94 -> 24.06 with them: it fills the table after round 1's wait, as before;
+  // profiles/r5s/ab_code_table_round1.txt)
+  constexpr bool kCodeLd = BT && C != 64;
+  CodeLd cld{0.0f, 0.0f, 0.0f};
+  if constexpr (kCodeLd) cld = obs_code_loads(st.tab, Rr, g.G, (int)(threadIdx.x & 255));
   load_tables_hot(smem, st.tab, a.g.G, Rr);
   // the sector rays' tables (pe_quad.hpp quad_rays): dist[R+1] = 1.0, one-hot rows
   static_assert(RM + 2 <= kOneHotF && kOneHotF + 16 <= 70, "ray tables inside dist[], below the done mask");
   if (threadIdx.x < 16) smem[kOneHotF + threadIdx.x] = (threadIdx.x >> 2) == (threadIdx.x & 3) ? 1.0f : 0.0f;
   if (threadIdx.x == 16) smem[Rr + 1] = 1.0f;
   if constexpr (BT) {
-    if (threadIdx.x < 256) ctab[threadIdx.x] = obs_code_value(st.tab, Rr, g.G, (int)threadIdx.x);
+    if (threadIdx.x < 256)
+      ctab[threadIdx.x] = kCodeLd ? obs_code_pick(cld, Rr, g.G, (int)threadIdx.x)
+                                  : obs_code_value(st.tab, Rr, g.G, (int)threadIdx.x);
   }
   if constexpr (RT) {  // the probe table (st.ldxy) into LDS: read from global memory in the ray
                        // loop, each 8-probe chunk was a vector load waited out with vmcnt(0)
@@ -2587,7 +2596,7 @@ __global__ __launch_bounds__(256) void pe_expand_codes_kernel(const Tables* tab,
                                                               const uint8_t* src, int64_t stride, float* obs,
                                                               float* rew, uint8_t* te, uint8_t* tr) {
   __shared__ float ctab[256];
-  ctab[threadIdx.x] = obs_code_value(tab, R, G, (int)threadIdx.x);
+  const CodeLd cld = obs_code_loads(tab, R, G, (int)threadIdx.x);  // (with the code loads: one round trip)
   const int b = blockIdx.y;
   const uint8_t* sb = src + (int64_t)b * stride;
   const int64_t nc = (int64_t)rows * D;  // codes per block
@@ -2603,6 +2612,7 @@ __global__ __launch_bounds__(256) void pe_expand_codes_kernel(const Tables* tab,
       const int64_t k = g0 + 256 * j;
       c[j] = 4 * k < nc ? *reinterpret_cast<const uint32_t*>(sb + 4 * k) : 0u;
     }
+    ctab[threadIdx.x] = obs_code_pick(cld, R, G, (int)threadIdx.x);
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kExpandPer; ++j) {
@@ -2622,6 +2632,7 @@ __global__ __launch_bounds__(256) void pe_expand_codes_kernel(const Tables* tab,
       }
     }
   } else {
+    ctab[threadIdx.x] = obs_code_pick(cld, R, G, (int)threadIdx.x);
     __syncthreads();
     for (int j = 0; j < kExpandPer; ++j) {
       const int64_t k = g0 + 256 * j;
@@ -3544,7 +3555,7 @@ int pe_step_codes(pe_handle* h, const void* actions, int32_t action_bytes, uint8
 
 int pe_obs_code_table(const pe_handle* h, float* table) {
   if (!h || !table) return fail(PE_ERR_ARG, "null argument");
-  // obs_code_value on the host tables: the same f32 quotients pe_create uploads
+  // obs_code_pick's table on the host tables: the same f32 quotients pe_create uploads
   const int R = h->g.R, G = h->g.G;
   for (int c = 0; c < 256; ++c) {
     float v = 0.0f;
