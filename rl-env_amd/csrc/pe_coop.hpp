@@ -754,8 +754,9 @@ struct ObsW<uint8_t> {
   __device__ __forceinline__ uint8_t pos(int x) const { return (uint8_t)(kCodePos + x); }
 };
 
-// The code table entry c in two halves for a kernel's first round: obs_code_loads issues
-// every candidate load unconditionally (with the round's other loads: a load inside the
+// The code table entry c from global memory in two halves (the expansion kernel and the
+// runtime-(C,R) byte-tile kernel's first round): obs_code_loads issues
+// every candidate load unconditionally (with the kernel's other loads: a load inside the
 // branches of a per-code `if` chain was waited out at once -- three dependent round trips in
 // the byte-coded kernels' first round, ~1.2 us, profiles/r5s/), obs_code_pick selects.
 struct CodeLd {
@@ -765,7 +766,21 @@ __device__ __forceinline__ CodeLd obs_code_loads(const Tables* tab, int R, int G
   const int px = c - kCodePos;
   return CodeLd{tab->dist[c <= R ? c : 0], tab->vis[(c - kCodeVis) & 15], tab->pos[px >= 0 && px < G ? px : 0]};
 }
-// The float of code c as one call (the far and C = 64 kernels: after their first round's wait).
+// The code table entry c from the step kernels' LDS tables (load_tables_hot's dist[0..R],
+// pos[0..G), vis[0..16), the kernel's dist[R+1] = 1.0 and one-hot zeros at kOneHotF):
+// one LDS read, no global load -- filled by each thread after a barrier that completes
+// round 1's LDS writes, read after the next one.
+__device__ __forceinline__ void ctab_from_lds(const float* smem, float* ctab, int R, int G, int c, int onehot_zero) {
+  const int f = c <= R + 1 ? c
+                           : ((c >= kCodeVis && c < kCodeVis + 16)
+                                  ? 328 + (c - kCodeVis)
+                                  : ((c >= kCodePos && c < kCodePos + G) ? 72 + (c - kCodePos) : onehot_zero));
+  ctab[c] = smem[f];
+}
+
+// The float of code c as one call: a per-code if-chain of global loads (each waited out at
+// once: three dependent round trips where a kernel's first round issues it -- the C = 64 and
+// far kernels, measured faster so, see pe_step_quad).
 __device__ __forceinline__ float obs_code_value(const Tables* tab, int R, int G, int c) {
   if (c <= R) return tab->dist[c];
   if (c == R + 1) return 1.0f;

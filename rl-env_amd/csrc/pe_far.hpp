@@ -337,9 +337,10 @@ __global__ __launch_bounds__(64 * kFarWaves, 4) void pe_step_far(StepArgs a) {
   load_tables_hot(smem, st.tab, g.G, R);
   if (threadIdx.x < 16) smem[kOneHotF + threadIdx.x] = (threadIdx.x >> 2) == (threadIdx.x & 3) ? 1.0f : 0.0f;
   if (threadIdx.x == 16) smem[R + 1] = 1.0f;
-  // (its code table after round 1's wait: the candidate loads issued with round 1, as the
-  // sector kernels do, measured 53.8 -> 55.4 us here -- three more live VGPRs in a kernel at
-  // its register cap; profiles/r5s/ab_code_table_round1.txt)
+  // (its code table after round 1's wait: the candidate loads issued with round 1 measured
+  // 53.8 -> 55.4 us here -- three more live VGPRs in a kernel at its register cap -- and the
+  // table filled from the LDS tables after the round-2 barrier 53.7 -> 54.4;
+  // profiles/r5s/ab_code_table_*.txt)
   ctab[threadIdx.x] = obs_code_value(st.tab, R, g.G, (int)threadIdx.x);  // (256 threads)
   Scal s = unpack(sw);
   const int64_t action = ash ? (int64_t)(((uint64_t)(uint32_t)ahi << 32) | (uint32_t)alo) : (int64_t)alo;

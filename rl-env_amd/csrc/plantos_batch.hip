@@ -1311,23 +1311,12 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
       qg1[j] = lgq[q < nq ? q : nq - 1];
     }
   }
-  // (BT: the code table's candidate loads go out with round 1, see obs_code_loads -- codes
-  // step 9.58 -> 9.25 us, 40x40/C48 28.84 -> 28.48; not at C = 64, whose synchronized step
-  // measured 23.94 -> 24.06 with them: it fills the table after round 1's wait, as before;
-  // profiles/r5s/ab_code_table_round1.txt)
-  constexpr bool kCodeLd = BT && C != 64;
-  CodeLd cld{0.0f, 0.0f, 0.0f};
-  if constexpr (kCodeLd) cld = obs_code_loads(st.tab, Rr, g.G, (int)(threadIdx.x & 255));
   load_tables_hot(smem, st.tab, a.g.G, Rr);
   // the sector rays' tables (pe_quad.hpp quad_rays): dist[R+1] = 1.0, one-hot rows
   static_assert(RM + 2 <= kOneHotF && kOneHotF + 16 <= 70, "ray tables inside dist[], below the done mask");
   if (threadIdx.x < 16) smem[kOneHotF + threadIdx.x] = (threadIdx.x >> 2) == (threadIdx.x & 3) ? 1.0f : 0.0f;
   if (threadIdx.x == 16) smem[Rr + 1] = 1.0f;
-  if constexpr (BT) {
-    if (threadIdx.x < 256)
-      ctab[threadIdx.x] = kCodeLd ? obs_code_pick(cld, Rr, g.G, (int)threadIdx.x)
-                                  : obs_code_value(st.tab, Rr, g.G, (int)threadIdx.x);
-  }
+
   if constexpr (RT) {  // the probe table (st.ldxy) into LDS: read from global memory in the ray
                        // loop, each 8-probe chunk was a vector load waited out with vmcnt(0)
     const uint4* src = reinterpret_cast<const uint4*>(st.ldxy);
@@ -1599,6 +1588,13 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // -> 9.65 us synchronized, 12.88 -> 12.43 us desynchronized; for the whole kernel
   // it slowed the synchronized step)
   if (wv == CW) __builtin_amdgcn_s_setprio(2);
+  // BT: the LDS code table from the LDS tables (complete at the barrier above; read after the
+  // done barrier).  It was a per-code if-chain of global loads in round 1, each waited out
+  // at once (three dependent round trips), then the candidate loads issued with round 1
+  // (profiles/r5s/ab_code_table_*.txt)
+  if constexpr (BT) {
+    if (threadIdx.x < 256) ctab_from_lds(smem, ctab, Rr, g.G, (int)threadIdx.x, kOneHotF + 1);
+  }
   // (Tried: the early record's state writes issued here, at the start of the compute
   // phase, instead of in the done path: the commit wave then waited for them before
   // re-using their data registers -- desynchronized 11.12 -> 12.05 us, synchronized
