@@ -3162,6 +3162,16 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   h->tile_codes = h->variant == V_QUAD_C64R6 || is_far(h->variant) ||
                           (is_quad(h->variant) && h->variant >= V_QUAD_RT_1W && C > kRtCMax)
                       ? 1 : 0;
+  // the runtime kernel with C <= 32 too, where its f32 tile holds fewer workgroups per CU than
+  // the byte tile and the batch needs more than one round of them (32x32 / C24 / R9: 54 KB, two
+  // per CU -- 65536 envs ran as two waves of workgroups, the second starting ~13 us in,
+  // profiles/r5s/stamps_g32.json); small batches keep the f32 tile (no expansion at the store)
+  if (!h->tile_codes && is_quad(h->variant) && h->variant >= V_QUAD_RT_1W) {
+    auto per_cu = [](size_t l) { return std::min<size_t>(4, (size_t)160 * 1024 / l); };
+    const size_t lf = quad_lds_bytes(g, false, true), lb = quad_lds_bytes(g, true, true);
+    const int64_t blocks = ((int64_t)n_envs + kQuadEnvs - 1) / kQuadEnvs;
+    if (per_cu(lb) > per_cu(lf) && blocks > (int64_t)prop.multiProcessorCount * (int64_t)per_cu(lf)) h->tile_codes = 1;
+  }
 #ifdef PE_DEBUG_KNOBS
   if (const char* tc = std::getenv("PE_TILE_CODES"))
     if (h->variant == V_QUAD_C16R6_1W || h->variant == V_QUAD_C64R6) h->tile_codes = std::atoi(tc) != 0;

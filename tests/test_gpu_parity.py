@@ -217,6 +217,8 @@ def test_rollout_parity_device_rng(name, n, steps):
 @pytest.mark.parametrize("name,desync,n", [("g20", False, 65536), ("g20", True, 65536), ("g64", False, 65536),
                                            ("g64", True, 65536), ("g64r32", True, 65536), ("g25", False, 65536),
                                            ("g25", True, 65536),
+                                           # the runtime kernel switched to the byte tile at full batch (C = 24)
+                                           ("g32", True, 65536),
                                            # BASELINE config 2 (16-env workgroups) and a 32-env-workgroup batch
                                            ("g20", False, 4096), ("g20", True, 4096), ("g20", True, 20000),
                                            # a ragged last block

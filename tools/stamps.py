@@ -4,7 +4,7 @@
 bench number -- read the SHARES and the timeline shape, not the length).
 
   python tools/stamps.py build                 # CPU: build/stamps/libplantos_hip_stamps.so
-  python tools/stamps.py run [--grid 20 --rays 16 --envs 65536] [--codes] [--desync] [--lib build/ab/lib_X.so]   # GPU
+  python tools/stamps.py run [--grid 20 --rays 16 --range 6 --envs 65536] [--codes] [--desync] [--lib build/ab/lib_X.so]   # GPU
 
 Stamps (lane 0 of each wave, 100 MHz = 10 ns ticks):
   0 entry  1 round-1 data in  2 round-2 loads landed + LDS written  3 after barrier
@@ -49,10 +49,10 @@ def run(argv):
     def arg(name, default):
         return int(argv[argv.index(name) + 1]) if name in argv else default
 
-    G, C, n = arg("--grid", 20), arg("--rays", 16), arg("--envs", 65536)
+    G, C, n, Rg = arg("--grid", 20), arg("--rays", 16), arg("--envs", 65536), arg("--range", 6)
     P, O = (10, 12) if G <= 32 else (100, 120)
     codes = "--codes" in argv  # the byte-coded step (pe_step_codes)
-    b = PlantOSBatch(n, grid_size=G, num_plants=P, num_obstacles=O, lidar_range=6, lidar_channels=C,
+    b = PlantOSBatch(n, grid_size=G, num_plants=P, num_obstacles=O, lidar_range=Rg, lidar_channels=C,
                      device="cuda:0", obs_codes=codes)
     desync = "--desync" in argv
     if desync:  # every env at its own step count (bench.py --desync)
