@@ -183,6 +183,16 @@ def measured_traffic(cfg, sha):
             "calibration": d.get("calibration")}
 
 
+def _symbol_bytetile(sym):
+    """True / False: the byte-coded obs tile of a pe_step_quad<C, R, ONEWORD, NW, BT, EPB>
+    symbol (its BT template argument; pe_step_far always has it); None: not parseable."""
+    import re
+    if "pe_step_far<" in sym:
+        return True
+    m = re.search(r"pe_step_quad<\s*\d+,\s*\d+,\s*(?:true|false),\s*\d+,\s*(true|false)", sym)
+    return None if m is None else m.group(1) == "true"
+
+
 def rocprof_kernel_ns(cfg, sha):
     """The step kernel's average launch duration (ns) from the committed rocprofv3
     --kernel-trace --stats summaries of this exact library and config
@@ -199,6 +209,11 @@ def rocprof_kernel_ns(cfg, sha):
             continue
         c = d.get("config", {})
         ns = d.get("avg_ns", d.get("stats_avg_ns"))
+        # the obs mode of the profiled kernel must be the benched one's: a byte-coded
+        # (codes / byte-tile) symbol never stands for an f32-tile kernel or vice versa
+        bt = _symbol_bytetile(d.get("kernel_symbol", ""))
+        if bt is not None and bt != ("bytetile" in str(cfg.get("kernel", ""))):
+            continue
         if ns and not d.get("desync") and d.get("lib_sha") == sha and all(c.get(k) == cfg.get(k) for k in keys):
             if best is None or os.path.basename(p).startswith("kstats_"):
                 best = (p, float(ns))
@@ -438,7 +453,24 @@ def gather_leg(torch, dist, device, shard, Kg, loop, world):
                 for t in range(64):
                     sh.unpack(sh.gathered(t & 1), out=loop.out)
             parts["expand_us"] = event_us(torch, capture_graph(torch, expands_only), 4, 64)
+            # the root's expansion at W = 8 ranks (BASELINE config 5): 8 copies of the slot in
+            # one [8, io_bytes] buffer -> the global f32 outputs of 8 x n envs, one launch
+            W8 = 8
+            src8 = sh.gathered(0).reshape(1, -1).repeat(W8, 1)
+            out8 = sh.new_outputs(W8)
+
+            def expands_w8():
+                for t in range(16):
+                    sh.unpack(src8, out=out8)
+            parts["expand_w8_us"] = event_us(torch, capture_graph(torch, expands_w8), 4, 16)
+            parts["expand_w8_bytes"] = {"read": int(src8.numel()),
+                                        "written": int(sum(t.numel() * t.element_size() for t in out8))}
+            del src8, out8
         parts["step_us"] = event_us(torch, capture_graph(torch, steps_only), 4, 64)
+        if "expand_w8_us" in parts:
+            parts["root_step_w8_us"] = parts["step_us"] + parts["expand_w8_us"]
+            parts["root_step_w8_note"] = ("implied per-step root cost at 8 ranks: its own codes step + the expansion "
+                                          "of 8 gathered blocks (the RCCL ingress overlaps both)")
     g_el, g_kms = timed(torch, dist, device, Kg, loop.step, chunk, graph, None if graph is not None else loop.finish)
     n = shard.n
     per_rank = shard.io_bytes()
@@ -705,18 +737,23 @@ def main():
             "lib_sha": sha,
         }
         # roofline of the step kernel: algorithmic bytes x envs / its average launch
-        # duration -- the committed rocprofv3 stats of this library and config where they
-        # exist (the judge's figure), else this run's back-to-back HIP-event measurement
+        # duration measured live in THIS run (HIP events on the launch stream around >= 2048
+        # back-to-back graph-replayed steps); the committed rocprofv3 stats of this library
+        # and config are a cross-check only, flagged when they disagree by more than 5 %
         rp = rocprof_kernel_ns(out["config"], sha)
-        k_us = rp["ns"] / 1e3 if rp else kern_us_events
+        k_us = kern_us_events
         achieved = B * n / (k_us * 1e-6) / 1e9
+        rp_us = rp["ns"] / 1e3 if rp else None
         out["roofline"] = {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "bytes_per_env_step": B,
             "kernel_us": k_us,
-            "kernel_us_source": (f"rocprofv3 --kernel-trace --stats average of this library ({rp['source']})" if rp
-                                 else "HIP events, >= 2048 back-to-back steps of captured graphs (this run)"),
-            "kernel_us_rocprof": rp["ns"] / 1e3 if rp else None,
+            "kernel_us_source": "HIP events, >= 2048 back-to-back steps of captured graphs (this run)",
+            "kernel_us_rocprof": rp_us,
+            "kernel_us_rocprof_source": (f"committed rocprofv3 --kernel-trace --stats average of this library and "
+                                         f"config ({rp['source']})" if rp else None),
+            "rocprof_agrees": (abs(k_us - rp_us) <= 0.05 * rp_us) if rp else None,
+            "frac_rocprof": B * n / (rp_us * 1e-6) / 1e9 / HBM_PEAK_GBPS if rp else None,
             "kernel_us_events": kern_us_events,
             "frac_events": B * n / (kern_us_events * 1e-6) / 1e9 / HBM_PEAK_GBPS,
             "kernel_us_window": kern_ms * 1e3, "frac_window": achieved_window / HBM_PEAK_GBPS,

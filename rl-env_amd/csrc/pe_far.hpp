@@ -74,11 +74,18 @@ struct FarQ {
 // LDS layout (floats): tables | the done path's scratch (quad_done_path: its staging
 // words, then one cooperative-reset scratch per wave; the lane path's LIDAR offsets) |
 // byte tile [64 x D] | code table [256]
+// The region also ends in the commit wave's park words (far_park_off, 6 x 64 floats): the
+// lane-per-env done path's LIDAR offsets (2CR bytes from its start, written by waves that
+// pass the done barrier while the commit wave may still read its park words) must stay
+// below them, so the region holds both side by side whatever the cooperative scratch.
 __host__ __device__ constexpr int far_scr_floats(int G, int WPR, int C, int R) {
   const int coop = 2 * (162 + kFarWaves * coop_scratch_words(G, WPR));
-  const int lane = (2 * C * R + 3) / 4;
+  const int lane = (2 * C * R + 3) / 4 + 6 * kQuadEnvs;
   return ((coop > lane ? coop : lane) + 3) & ~3;
 }
+static_assert(far_scr_floats(33, kCoopWPR, 64, 32) - 6 * kQuadEnvs >= (2 * 64 * 32 + 3) / 4 &&
+                  far_scr_floats(64, kCoopWPR, 64, 32) - 6 * kQuadEnvs >= (2 * 64 * 32 + 3) / 4,
+              "far kernel: the park words overlap the lane path's LIDAR offsets");
 __host__ __device__ constexpr int far_tile_off(int G, int WPR, int C, int R) {
   return kTabFloats + far_scr_floats(G, WPR, C, R);
 }

@@ -307,13 +307,17 @@ def test_determinism_and_sharding_equivalence():
         x.close()
 
 
-@pytest.mark.parametrize("name", ["g20", "g16c40", "g8r20"])
-@pytest.mark.parametrize("n", [1, 63, 65, 1000])
+@pytest.mark.parametrize("name,n", [(nm, k) for nm in ("g20", "g16c40", "g8r20") for k in (1, 63, 65, 1000)] +
+                         [("g64r32", k) for k in (1, 63, 65)])
 def test_ragged_batch_sizes(n, name):
     """int64 actions (8-byte action words) and partial workgroups, through the sector
-    kernel and both ray paths of the one-wave-per-env kernel"""
+    kernel, both ray paths of the one-wave-per-env kernel and the far kernel (g64r32:
+    its off-map quadrant rows are loaded unclamped, so a one-env batch reads the slack
+    pe_create keeps around the grid array on both sides)"""
     cfg = CFG[name]
     b = make(cfg, n, seed=3)
+    if name == "g64r32":
+        assert b.kernel_name == KERNELS[name]
     ov = OracleVec(cfg, np.arange(n), 3)
     for t in range(30):
         a = np.array([O.synth_action(11, e, t) for e in range(n)], np.int64)
