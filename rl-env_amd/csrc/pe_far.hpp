@@ -106,9 +106,15 @@ __host__ __device__ constexpr int far_stage_units(int G, int WPR, int C) {
   return pf_stage_units(G, WPR, ((5 * C + 27) + 15) & ~15, false);
 }
 __host__ __device__ constexpr int far_stage_off(int G, int WPR, int C, int R) { return far_ctab_off(G, WPR, C, R) + 256; }
+// (round 6) after the record: the env's current grid rows for its terminal info, register-
+// staged by the info wave in round 2 (pe_step_far info_reg), then one unit of the done env's
+// post-step scalars and one of its wfix, parked by the commit wave for the info wave
+__host__ __device__ constexpr int far_info_park_unit(int G, int WPR, int C) {
+  return far_stage_units(G, WPR, C) + pf_grid_units(G, WPR);
+}
 __host__ __device__ constexpr int far_lds_floats(int G, int WPR, int C, int R) {
   // (whole 64-unit LDS-DMA instructions: every lane of the last one writes its unit)
-  return far_stage_off(G, WPR, C, R) + 4 * 64 * ((far_stage_units(G, WPR, C) + 63) / 64);
+  return far_stage_off(G, WPR, C, R) + 4 * 64 * ((far_info_park_unit(G, WPR, C) + 2 + 63) / 64);
 }
 
 // Quadrant W's rays for this lane's env at the post-move position (xp, yp): first hit
@@ -307,10 +313,12 @@ __device__ __forceinline__ bool far_commit(const StepArgs& a, int64_t e, Scal& s
 template <int C, int R>
 __device__ __attribute__((noinline)) uint4 far_done(const void* ka, int tile_off, int lane, int wv, int64_t e0,
                                                     bool done, uint4 sp, double ret, int ndone, bool wfix,
-                                                    const float* ctab, const float* stage, bool stage_info) {
+                                                    const float* ctab, const float* stage, bool stage_info,
+                                                    bool info_iw, int park_unit) {
   constexpr int D = 5 * C + 27;
-  return quad_done_path<kFarWaves, false, (D + 63) / 64, true>(ka, tile_off, C, R, lane, wv, kFarWaves - 1, e0, done,
-                                                               sp, ret, ndone, wfix, ctab, stage, stage_info);
+  return quad_done_path<kFarWaves, false, (D + 63) / 64, true>(
+      ka, tile_off, C, R, lane, wv, kFarWaves - 1, e0, done, sp, ret, ndone, wfix, ctab, stage, stage_info, -1,
+      nullptr, nullptr, -1, false, info_iw, stage ? stage + 4 * park_unit : nullptr);
 }
 
 template <int C, int R>
@@ -376,11 +384,23 @@ __global__ __launch_bounds__(64 * kFarWaves, 4) void pe_step_far(StepArgs a) {
   const bool stage_ok = a.pf.scal && quad_coop(a, 1) && e0 + LS <= a.n;  // full block: every lane live
   constexpr bool stage_info = false;  // (see far_stage_units)
   int npred = 0;
+  // (round 6) the predicted env's current grid rows for its terminal info, register-staged
+  // by the info wave (two 16-B units per lane, written to LDS before the march): the info
+  // wave then writes the terminal info beside the commit wave's reset, instead of the commit
+  // wave loading the rows after the done barrier (a round trip on the one-done block's path)
+  const int ng_s = pf_grid_units(g.G, g.WPR);
+  const bool info_reg = PE_BT_INFO_REG && stage_ok && !st.cur && a.tinfo != nullptr && ng_s <= 128;
+  uint4 iq0 = make_uint4(0u, 0u, 0u, 0u), iq1 = iq0;
   if (stage_ok) {
     const uint64_t pm = __ballot(s.step + 1 >= a.rl.max_steps);
     npred = __popcll(pm);
     if (wv == CW && npred == 1)
       pf_stage_issue(a.pf, st, g, e0 + (__ffsll((unsigned long long)pm) - 1), stage, lane, stage_info);
+    if (info_reg && wv == kQuadInfoWave && npred == 1) {
+      const uint4* src = reinterpret_cast<const uint4*>(st.grid + (e0 + (__ffsll((unsigned long long)pm) - 1)) * g.gstride);
+      iq0 = src[lane < ng_s ? lane : ng_s - 1];
+      iq1 = src[lane + 64 < ng_s ? lane + 64 : ng_s - 1];
+    }
   }
   const int vw0 = (4 * m.ybv) >> 5, vo = (4 * m.ybv) & 31;
   uint32_t cv[2][3][2];  // [slice row t][candidate k][word]
@@ -421,6 +441,11 @@ __global__ __launch_bounds__(64 * kFarWaves, 4) void pe_step_far(StepArgs a) {
   // one).  (The candidate slice rows and the rays' rows may see the new bytes: the slice
   // centre is rebuilt from nib, the watered cell's fix is idempotent.)
   asm volatile("s_barrier" ::"v"(vt), "v"(gt), "v"(gc) : "memory");
+  if (info_reg && wv == kQuadInfoWave && npred == 1) {  // (into LDS before the march: no registers across it)
+    uint4* d = reinterpret_cast<uint4*>(stage) + far_stage_units(g.G, g.WPR, C);
+    if (lane < ng_s) d[lane] = iq0;
+    if (lane + 64 < ng_s) d[lane + 64] = iq1;
+  }
   uint8_t* row = rows + lane * D;
   bool done = false, wfix = false;
   uint32_t* park = reinterpret_cast<uint32_t*>(smem + far_park_off(g.G, g.WPR, C, R));
@@ -471,9 +496,18 @@ __global__ __launch_bounds__(64 * kFarWaves, 4) void pe_step_far(StepArgs a) {
     }
   }
   // ---- DummyVecEnv auto-reset (rare): the commit wave's done mask in dist[70..71]
+  const int park_unit = far_info_park_unit(g.G, g.WPR, C);
   if (wv == CW) {
     const uint64_t dm = __ballot(done);
     if (lane == 0) reinterpret_cast<uint64_t*>(smem)[35] = dm;
+    if (info_reg && npred == 1 && __popcll(dm) == 1 && done) {  // the one done env's scalars for the info wave
+      float* pk = stage + 4 * park_unit;  // (from the commit wave's park words: no registers across the march)
+      pk[0] = __int_as_float((int)park[lane]);
+      pk[1] = __int_as_float((int)park[64 + lane]);
+      pk[2] = __int_as_float((int)park[128 + lane]);
+      pk[3] = __int_as_float((int)park[192 + lane]);
+      pk[4] = __int_as_float((int)wfix);
+    }
   }
   // the block barrier without a memory fence (see pe_step_quad)
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -492,7 +526,7 @@ __global__ __launch_bounds__(64 * kFarWaves, 4) void pe_step_far(StepArgs a) {
     }
     const bool staged = stage_ok && npred == 1 && ndone == 1;  // then the done env is the predicted one
     sp = far_done<C, R>(kernargs(), tile_off, lane, wv, e0, done, sp, rv, ndone, wfix, ctab, staged ? stage : nullptr,
-                        staged && stage_info);
+                        staged && stage_info, staged && info_reg, park_unit);
   }
   if (wv == CW) __builtin_amdgcn_s_waitcnt(0x0F70);  // tracked vmcnt(0): no wait inside the store loop
 #if defined(PE_FAR_PROBE) && PE_FAR_PROBE == 2  // timing probe (no obs): no tile store

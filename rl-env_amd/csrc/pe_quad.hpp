@@ -202,6 +202,73 @@ __device__ __forceinline__ void quad_rays_rt(const uint64_t* lrow, const uint32_
   }
 }
 
+// Runtime-(C, R) sector rays from a register window (round 6): the wave's sector rows
+// dx in [LO, LO + NROWS) -- at most kRtRegRows, at most 16 columns dy in [DLO, DLO + 15]
+// -- each read once from LDS and shifted by the lane's column offset into one 32-bit
+// word (window column dy - DLO at bits 2(dy - DLO)); a probe is then the word at a
+// wave-uniform index (VGPR indexing: s_set_gpr_idx_on + v_mov), one v_bfe at a uniform
+// bit offset and one v_lshl_or into the packed codes -- 3 VALU instead of ~5.5 (an
+// address add, a shift-amount add, the LDS read, a 64-bit shift, the mask and the pack).
+// The probe entries (row index | bit offset << 8) and the sector header {LO, DLO,
+// NROWS, ok} come through the scalar cache (constant address space: s_load), so their
+// decode is SALU.  pe_create builds both; a sector whose rows or columns do not fit
+// (ok == 0, e.g. uneven sectors of some C not a multiple of 4) takes quad_rays_rt.
+constexpr int kRtRegRows = 15;  // R + 1 rows of a quadrant at R <= 14
+typedef const __attribute__((address_space(4))) uint32_t* rt_cptr;
+template <typename OT>
+__device__ __forceinline__ void quad_rays_rt_reg(const uint64_t* lrow, rt_cptr hdr, rt_cptr ent, int i0, int i1,
+                                                 int R, int lane, int kc, int sh, bool watered, OT* row,
+                                                 const float* tdist) {
+  const int RP = (R + 7) & ~7;
+  const int LO = (int)hdr[0], DLO = (int)hdr[1], NR = (int)hdr[2];
+  const uint32_t kNZ = 0x55555555u & ((1u << (2 * R)) - 1u);  // R <= 14
+  const float4* tone = reinterpret_cast<const float4*>(tdist + kOneHotF);
+  const int shw = sh + 2 * (DLO + R);  // the lane's bit of window column DLO in its LDS row word (< 64)
+  uint32_t w[kRtRegRows];
+#pragma unroll
+  for (int j = 0; j < kRtRegRows; ++j) {  // (rows past NR: the last row again, never probed)
+    const int jj = j < NR ? j : NR - 1;
+    w[j] = (uint32_t)(lrow[(kc + LO + jj) * kQuadEnvs + lane] >> shw);
+  }
+  const uint32_t origin = (uint32_t)(-LO) | ((uint32_t)(-2 * DLO) << 8);  // the entry of probe (0, 0)
+  for (int i = i0; i < i1; ++i) {
+    rt_cptr e = ent + i * RP;
+    uint32_t pk = 0u;
+    int r0 = 0;
+    for (; r0 + 8 <= R; r0 += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t v = e[r0 + j];
+        pk |= __builtin_amdgcn_ubfe(w[v & 31u], (v >> 8) & 31u, 2) << (2 * (r0 + j));
+      }
+    }
+    for (; r0 < R; ++r0) {
+      const uint32_t v = e[r0];
+      pk |= __builtin_amdgcn_ubfe(w[v & 31u], (v >> 8) & 31u, 2) << (2 * r0);
+    }
+    const uint32_t nz = ((pk | (pk >> 1)) & kNZ) | (1u << (2 * R));
+    const int f = __builtin_ctz(nz);        // 2r of the first hit, 2R if none
+    int ent_code = (int)((pk >> f) & 3u);   // its code (EMPTY if none)
+    if (watered && f == 0 && e[0] == origin) ent_code &= 2;  // the watered rover cell: THIRSTY -> HYD
+    if constexpr (std::is_same<OT, float>::value) {
+      const float dv = tdist[(f >> 1) + 1];
+      const float4 ov = tone[ent_code];
+      row[5 * i] = dv;
+      row[5 * i + 1] = ov.x;
+      row[5 * i + 2] = ov.y;
+      row[5 * i + 3] = ov.z;
+      row[5 * i + 4] = ov.w;
+    } else {
+      row[5 * i] = (uint8_t)((f >> 1) + 1);
+      const uint32_t oh = (uint32_t)(R + 1) << (8 * ent_code);
+      row[5 * i + 1] = (uint8_t)oh;
+      row[5 * i + 2] = (uint8_t)(oh >> 8);
+      row[5 * i + 3] = (uint8_t)(oh >> 16);
+      row[5 * i + 4] = (uint8_t)(oh >> 24);
+    }
+  }
+}
+
 // Wave-uniform dispatch of the sector code (wv comes from readfirstlane).
 template <int C, int R, int NW, int W = 0, typename T>
 __device__ __forceinline__ void sector_rays(int wv, const uint64_t* lrow, int lane, int kc, int sh, bool watered,

@@ -539,6 +539,16 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
 #ifndef PE_BT_EARLY
 #define PE_BT_EARLY 1  // the byte-coded one-word kernel loads a predicted single truncation's record early (A/B: 0)
 #endif
+#ifndef PE_REG_STAGE
+#define PE_REG_STAGE 1  // f32 kernels without the early record: a predicted single truncation's record
+                        // register-staged into LDS during round 2 (A/B: 0)
+#endif
+#ifndef PE_RT_REG
+#define PE_RT_REG 1  // runtime sector kernel: rays from a per-wave register window (A/B: 0, the LDS-table form)
+#endif
+#ifndef PE_BT_INFO_REG
+#define PE_BT_INFO_REG 1  // byte-coded LDS-DMA kernels: the info rows register-staged by the info wave (A/B: 0)
+#endif
 #ifndef PE_BT_STAGE_MIN_C
 #define PE_BT_STAGE_MIN_C 64  // byte-coded kernels stage the predicted record by LDS-DMA from this C on (A/B: 0)
 #endif
@@ -661,7 +671,12 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
                                                 bool stage_info = false, int64_t e_early = -1,
                                                 const PfLoad<ONEWORD ? 1 : kCoopWPR, KD>* early = nullptr,
                                                 const Row4<ONEWORD ? 1 : kCoopWPR>* early_rows = nullptr,
-                                                int64_t e_info = -1) {
+                                                int64_t e_info = -1, bool stage_reg = false, bool info_iw = false,
+                                                const float* ipark = nullptr) {
+  // stage_reg: `stage` was written by register-staged copies before the window barrier
+  // (pe_step_quad kRegStage), not by LDS-DMA: nothing to wait for.  info_iw: the env's
+  // terminal-info rows were register-staged into `stage` (after the record) by the info
+  // wave (kQuadInfoWave), which writes the terminal info beside the commit wave's reset
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const StepArgs& a = *reinterpret_cast<const StepArgs*>(ka);
   const Geo& g = a.g;
@@ -760,9 +775,9 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         }
         // with the curriculum the commit stored this env's rows: they must land before
         // the info reads them and the reset rewrites them
-        if (st.cur || stage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (stage: the LDS-DMA landed)
+        if (st.cur || (stage && !stage_reg)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (stage: the LDS-DMA landed)
         PE_DSTAMP(1);
-        if (a.tinfo) {
+        if (a.tinfo && !info_iw) {  // (register-staged info rows: the info wave's)
           if (stage_info)  // the env's rows came with the record
             coop_info_store<MAXW>(st, g,
                                   pf_stage_rows<MAXW>(reinterpret_cast<const uint64_t*>(
@@ -806,6 +821,23 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
                                    (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(pk[3])));
       const int wf = __builtin_amdgcn_readfirstlane(__float_as_int(pk[4]));
       coop_info_store<MAXW>(st, g, *early_rows, unpack(spk), a.tinfo + e_info * PE_NINFO, lane, wf, ltab);
+    } else if (info_iw && a.tinfo && wv == kQuadInfoWave) {
+      // the terminal info of the staged env (the block's one done env: its truncation was
+      // predicted) by the info wave from its rows register-staged in round 2 and its
+      // post-step scalars parked by the commit wave (kInfoParkF; ipark: the far kernel's slot)
+      const uint64_t dmw = reinterpret_cast<const uint64_t*>(smem)[35];
+      const int64_t el = e0 + (__ffsll((unsigned long long)dmw) - 1);
+      const float* pk = ipark ? ipark : smem + kInfoParkF;
+      const uint4 spk = make_uint4((uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(pk[0])),
+                                   (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(pk[1])),
+                                   (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(pk[2])),
+                                   (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(pk[3])));
+      const int wf = __builtin_amdgcn_readfirstlane(__float_as_int(pk[4]));
+      coop_info_store<MAXW>(st, g,
+                            pf_stage_rows<MAXW>(reinterpret_cast<const uint64_t*>(
+                                                    stage + 4 + 4 * pf_grid_units(g.G, g.WPR) + a.pf.ostride / 4),
+                                                g, lane),
+                            unpack(spk), a.tinfo + el * PE_NINFO, lane, wf, ltab);
     }
     __syncthreads();  // the fresh obs row is in the tile
     __builtin_amdgcn_s_waitcnt(0x0F70);  // see the end of the path below
@@ -1086,8 +1118,20 @@ __device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* 
     const int sh = 2 * (yp - m.yb);
     const int vs = 4 * (yp - m.ybv);
     if constexpr (RT) {
-      const uint32_t* ltab = reinterpret_cast<const uint32_t*>(reinterpret_cast<const float*>(rows) + quad_rtab_off(Cr, BT));
-      quad_rays_rt<OT>(lrow, ltab, wv * Cr / NW, (wv + 1) * Cr / NW, Rr, lane, kc, sh, watered, row, tdist);
+      // the register-window form where pe_create found the wave's sector fits it (its header's
+      // ok word, after the LDS-form table in st.ldxy), else the LDS-table form
+      const uint32_t* gt = reinterpret_cast<const uint32_t*>(st.ldxy) + Cr * ((Rr + 7) & ~7);
+      const rt_cptr hdr = (rt_cptr)(gt + 4 * wv);
+#if PE_RT_REG
+      if (hdr[3]) {
+        quad_rays_rt_reg<OT>(lrow, hdr, (rt_cptr)(gt + 16), wv * Cr / NW, (wv + 1) * Cr / NW, Rr, lane, kc, sh, watered,
+                             row, tdist);
+      } else
+#endif
+      {
+        const uint32_t* ltab = reinterpret_cast<const uint32_t*>(reinterpret_cast<const float*>(rows) + quad_rtab_off(Cr, BT));
+        quad_rays_rt<OT>(lrow, ltab, wv * Cr / NW, (wv + 1) * Cr / NW, Rr, lane, kc, sh, watered, row, tdist);
+      }
     } else {
       sector_rays<C, R, NW>(wv, lrow, lane, kc, sh, watered, row, tdist);
     }
@@ -1165,6 +1209,9 @@ __device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* 
 #if defined(PE_PROBE_VISIDLE)  // (timing / traffic probe, wrong results: the byte into the idle slot)
           st_wt(reinterpret_cast<uint8_t*>(vis_env(st, g, e, s.episode ^ 1u) + (int64_t)m.nx * g.NW) + b,
                 (uint8_t)(wnew >> (4 * (2 * b - m.ybv))));
+#elif defined(PE_VIS_PLAIN)  // (A/B: a write-back byte store, merged into the L2 line round 2 read)
+          *(reinterpret_cast<uint8_t*>(vis_env(st, g, e, s.episode) + (int64_t)m.nx * g.NW) + b) =
+              (uint8_t)(wnew >> (4 * (2 * b - m.ybv)));
 #else
           st_wt(reinterpret_cast<uint8_t*>(vis_env(st, g, e, s.episode) + (int64_t)m.nx * g.NW) + b,
                 (uint8_t)(wnew >> (4 * (2 * b - m.ybv))));
@@ -1319,6 +1366,9 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
 
   if constexpr (RT) {  // the probe table (st.ldxy) into LDS: read from global memory in the ray
                        // loop, each 8-probe chunk was a vector load waited out with vmcnt(0)
+    // (the LDS form's table: the sectors the register window does not take; round 6: the
+    // copy's loads issued with round 1's, one unit per thread, measured slower -- 32x32/C24/R9
+    // 17.05 -> 17.39 us, 40x40/C48/R8 28.57 -> 29.1, profiles/r6c/)
     const uint4* src = reinterpret_cast<const uint4*>(st.ldxy);
     uint4* dst = reinterpret_cast<uint4*>(smem + tail_off);
     for (int k = threadIdx.x; k < Cr * ((Rr + 7) & ~7) / 4; k += blockDim.x) dst[k] = src[k];  // (u32 entries)
@@ -1355,9 +1405,22 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
     pm = __ballot(s.step + 1 >= rl.max_steps);
     npred = __popcll(pm);
   }
+  // (round 6) the env's current grid rows for its terminal info, when they do not fit the
+  // record's LDS-DMA instructions (64x64, the runtime kernel's larger grids): register-staged
+  // by the info wave (two 16-B units per lane) into the staging region after the record,
+  // so that the info wave writes the terminal info beside the commit wave's reset instead
+  // of the commit wave loading them after the done barrier (a round trip on its path)
+  const int ng_s = pf_grid_units(g.G, g.WPR);
+  const bool info_reg = BT && PE_BT_INFO_REG && stage_ok && !stage_info && !st.cur && a.tinfo != nullptr && ng_s <= 128;
+  uint4 iq0 = make_uint4(0u, 0u, 0u, 0u), iq1 = iq0;
   auto stage_issue = [&]() {
     if (BT && wv == CW && npred == 1)
       pf_stage_issue(a.pf, st, g, e0 + (__ffsll((unsigned long long)pm) - 1), stage, lane, stage_info);
+    if (BT && info_reg && wv == kQuadInfoWave && npred == 1) {
+      const uint4* src = reinterpret_cast<const uint4*>(st.grid + (e0 + (__ffsll((unsigned long long)pm) - 1)) * g.gstride);
+      iq0 = src[lane < ng_s ? lane : ng_s - 1];
+      iq1 = src[lane + 64 < ng_s ? lane + 64 : ng_s - 1];
+    }
   };
   quad_move_cells<ONEWORD>(m, s, g.G);
 
@@ -1405,6 +1468,57 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
       }
     }
   }
+  // Register-staged record (round 6; the f32 kernels that have neither the early record
+  // nor LDS-DMA staging: the multi-word rows -- 25x25, 21x21 -- the runtime-(C, R) f32
+  // kernel and the 16 / 32-env small-batch shapes).  A block whose ONLY env to truncate
+  // this step is known from its step count (:177) has the commit wave load that env's
+  // prefetched record -- scalars, grid rows, obs row: one 16-B unit per lane, the layout
+  // of pf_stage_issue -- and the info wave the env's current grid rows, right after round
+  // 2's loads; both are written into the LDS staging region after round 2's LDS writes,
+  // so they hold 4 VGPRs through round 2 only (the early record's registers live across
+  // the compute phase spilled the multi-word kernel, at its 128-VGPR cap), and the single-
+  // done path makes no memory round trip: the commit wave takes the staged record, the
+  // info wave writes the terminal info from the staged rows beside it.
+  // (not the 16 / 32-env small-batch shapes: 4096 envs synchronized 4.43 -> 4.62 us for
+  // desynchronized 6.38 -> 6.30, profiles/r6c/)
+  constexpr bool kRegStage = PE_REG_STAGE && !kEarlyRec && !BT && NW > kQuadInfoWave && EPB == kQuadEnvs;
+  // (the staging outcome goes to LDS -- kRsFlagF, written by the commit wave every launch --
+  // and the done env's scalars are parked after the compute phase: no SGPRs live across it)
+  constexpr int kRsFlagF = kInfoParkF + 5;
+  static_assert(!(kRegStage || BT) || (RM + 2 <= kInfoParkF && kRsFlagF + 1 <= kOneHotF), "info park words inside dist[]");
+  bool rs_on = false, rs_info = false;  // (wave-uniform; identical in the commit and the info wave)
+  int64_t e_rs = -1;
+  uint4 rq = make_uint4(0u, 0u, 0u, 0u);
+  int rs_u = 0, rs_n = 0;  // this lane's staging unit, the wave's unit count
+  if constexpr (kRegStage) {
+    if ((wv == CW || wv == kQuadInfoWave) && a.pf.scal && a.autoreset && !st.cur && quad_coop(a, 1)) {
+      const uint64_t pmk = __ballot(live && s.step + 1 >= rl.max_steps);
+      const uint64_t pmu = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pmk) |
+                           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pmk >> 32)) << 32);
+      const int ng = pf_grid_units(g.G, g.WPR), no = (int)a.pf.ostride / 16;
+      if (__popcll(pmu) == 1 && 1 + ng + no <= 64) {
+        rs_on = true;
+        rs_info = a.tinfo != nullptr;
+        e_rs = e0 + (__ffsll((unsigned long long)pmu) - 1);
+        rs_n = wv == CW ? 1 + ng + no : (rs_info ? ng : 0);
+        rs_u = (wv == CW ? 0 : 1 + ng + no) + (lane < rs_n ? lane : rs_n - 1);
+      }
+    }
+  }
+  auto rs_issue = [&]() {
+    if (kRegStage && rs_n > 0) {
+      const int ng = pf_grid_units(g.G, g.WPR);
+      const int u = rs_u;
+      const uint4* src;
+      if (wv == CW)
+        src = u == 0 ? reinterpret_cast<const uint4*>(a.pf.scal + e_rs)
+                     : (u <= ng ? reinterpret_cast<const uint4*>(a.pf.grid + e_rs * g.gstride) + (u - 1)
+                                : reinterpret_cast<const uint4*>(pf_obs_row(a.pf, e_rs)) + (u - 1 - ng));
+      else
+        src = reinterpret_cast<const uint4*>(st.grid + e_rs * g.gstride) + (u - (1 + ng + (int)a.pf.ostride / 16));
+      rq = *src;
+    }
+  };
   // ---- round 2: window rows of env le -> LDS [row][env] (loader role)
   uint32_t eo = 0u, en = 0u;
   if (llive) {
@@ -1440,6 +1554,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
         }
       }
       stage_issue();
+      rs_issue();  // (after round 2's loads: their waits stay as they were)
       if constexpr (kGridR1) {
         // the block's rows (pairs 2q, 2q+1) inside the window, then the off-map rows
         const int nq = (int)(g.gstride >> 1);
@@ -1530,6 +1645,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
         vhi[j] = vb[(int64_t)xc * g.NW + 1];  // vw + 1 < NW always (one spare word per row)
       }
       stage_issue();
+      rs_issue();  // (after round 2's loads: their waits stay as they were)
 #pragma unroll
       for (int j = 0; j < JG; ++j) {
         const int k = sub + LT * j;
@@ -1557,6 +1673,17 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
         }
       }
     }
+  } else {
+    rs_issue();  // (a lane whose loader env is past the batch end: its staging unit all the same)
+  }
+  // the register-staged units into the LDS staging region (after round 2's LDS writes:
+  // the wait for them is the last of the round)
+  if (kRegStage && rs_n > 0 && lane < rs_n) reinterpret_cast<uint4*>(stage)[rs_u] = rq;
+  if (kRegStage && wv == CW && lane == 0) smem[kRsFlagF] = __int_as_float((int)rs_on | ((int)rs_info << 1));
+  if (BT && info_reg && wv == kQuadInfoWave && npred == 1) {
+    uint4* d = reinterpret_cast<uint4*>(stage) + 1 + ng_s + (int)a.pf.ostride / 16;
+    if (lane < ng_s) d[lane] = iq0;
+    if (lane + 64 < ng_s) d[lane + 64] = iq1;
   }
   // what the state commit needs beyond the window rows (lane = env): only in the
   // curriculum / injected-state modes (the visit and grid words it rewrites are
@@ -1612,6 +1739,20 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
       smem[kInfoParkF + 4] = __int_as_float((int)wfix);
     }
   }
+  if constexpr (kRegStage || (BT && !kEarlyRec && NW > kQuadInfoWave)) {  // a block's one done env's post-step
+                                                                           // scalars for the info wave (as kInfoW)
+    if (wv == CW) {
+      const uint64_t dm1 = __ballot(done);
+      if (__popcll(dm1) == 1 && done) {
+        const uint4 pk = pack(s);
+        smem[kInfoParkF] = __int_as_float((int)pk.x);
+        smem[kInfoParkF + 1] = __int_as_float((int)pk.y);
+        smem[kInfoParkF + 2] = __int_as_float((int)pk.z);
+        smem[kInfoParkF + 3] = __int_as_float((int)pk.w);
+        smem[kInfoParkF + 4] = __int_as_float((int)wfix);
+      }
+    }
+  }
   PE_STAMP(4);
   // ---- DummyVecEnv auto-reset (rare): commit wave, after the whole obs row is in LDS
   // any env of the block done (the usual answer: no)?  The commit wave's done mask
@@ -1644,9 +1785,13 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   const int64_t valid = a.n - e0 < EPB ? a.n - e0 : EPB;
   if (__builtin_expect(any_done, 0)) {  // cold: laid out after the hot path
     const bool staged = stage_ok && npred == 1 && ndone == 1;  // then the done env is the predicted one
+    // (register-staged: the single done env is the predicted one likewise)
+    const int rsf = kRegStage ? __builtin_amdgcn_readfirstlane(__float_as_int(smem[kRsFlagF])) : 0;
+    const bool rstaged = kRegStage && (rsf & 1) && ndone == 1;
     const uint4 ns = quad_done_path<NW, ONEWORD, (5 * CM + 27 + 63) / 64, BT>(
         kernargs(), tile_off, Cr, Rr, lane, wv, CW, e0, done, pack(s), ret, ndone, wfix, ctab,
-        staged ? stage : nullptr, staged && stage_info, e_early, &epl, &eir, e_info);
+        (staged || rstaged) ? stage : nullptr, (staged && stage_info) || (rstaged && (rsf & 2)), e_early, &epl, &eir,
+        e_info, rstaged, (rstaged && (rsf & 2)) || (staged && info_reg));
     s = unpack(ns);
   }
   // the obs tile goes out through the waves other than the commit wave: its state
@@ -2746,7 +2891,14 @@ size_t quad_lds_bytes(const Geo& g, bool codes, bool rt) {
   const size_t off = (size_t)((kTabFloats + (2 * g.R + 3) * kQuadEnvs * 2 + 7 * kQuadEnvs + 3) & ~3) +
                      (rt ? (size_t)quad_rtab_floats(g.C, g.R) : 0);  // (+ the runtime kernel's probe table)
   // + the single-done record's LDS-DMA staging region (pe_coop.hpp pf_stage_issue)
-  const size_t stage = (size_t)pf_stage_bytes(g.G, g.WPR, (int)pf_ostride(g, codes));
+  size_t stage = (size_t)pf_stage_bytes(g.G, g.WPR, (int)pf_ostride(g, codes));
+  // (f32 kernels: the register-staged record and, beside it, the info wave's rows --
+  // pe_step_quad kRegStage stages whenever the record fits one unit per lane)
+  const int ng = pf_grid_units(g.G, g.WPR), no = (int)pf_ostride(g, codes) / 16;
+  if (!codes && 1 + ng + no <= 64) stage = std::max(stage, (size_t)((1 + 2 * ng + no + 63) / 64) * 1024);
+  // (byte-coded kernels that stage by LDS-DMA: the record, then the info wave's rows)
+  if (codes && (rt || g.C >= PE_BT_STAGE_MIN_C) && ng <= 128)
+    stage = std::max(stage, (size_t)((1 + 2 * ng + no + 63) / 64) * 1024);
   if (codes)  // byte tile + code table (quad_ctab_off)
     return sizeof(float) * (off + (size_t)((kQuadEnvs * g.D + 15) / 16) * 4 + 256) + stage;
   return sizeof(float) * (off + (size_t)kQuadEnvs * g.D) + stage;
@@ -3191,11 +3343,14 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   }
   if (h->tile_codes) {
     h->quad_waves = 4;
+    // (not the byte-coded C16 kernel -- config 5's codes step: its quarters started apart
+    // cost it ~0.9 us desynchronized, 11.68 -> 10.75 us without, profiles/r6c/ab_codesstag;
+    // the runtime byte-tile kernel keeps it: 32x32/C24/R9 17.0 -> 18.1 us without)
     // all 1024 workgroups of a 65536-env batch are resident at once (4 per CU) and
     // would run their load, compute and 89-KB store phases in lockstep: starting the
     // grid's quarters ~0.85 us apart overlaps one quarter's stores with the next
     // one's loads (64x64 / 64 rays, same-box: 28.7 -> 26.3 us; 2x that: 27.0)
-    h->stagger = 4;
+    h->stagger = h->variant == V_QUAD_C16R6_1W ? 0 : 4;
   }
 #ifdef PE_DEBUG_KNOBS
   if (const char* sg = std::getenv("PE_STAGGER")) h->stagger = std::atoi(sg);
@@ -3279,7 +3434,9 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   const int RP = (R + 7) & ~7;
   const bool wave_aln = h->variant == V_GENERIC && wave_aln_ok(G, R, g.WPR);  // pe_step_wave<., true>
   const bool rt_tab = h->variant == V_QUAD_RT_1W || h->variant == V_QUAD_RT;  // u32 probe entries (quad_rays_rt)
-  const size_t o_ldxy = carve(wave_aln ? ((size_t)C * RP * 3 + 15) & ~(size_t)15 : (size_t)C * RP * (rt_tab ? 4 : 2));
+  // (rt_tab: the LDS-form entries, then the register-window header [4][4] and entries, pe_quad.hpp)
+  const size_t o_ldxy = carve(wave_aln ? ((size_t)C * RP * 3 + 15) & ~(size_t)15
+                                       : (rt_tab ? (2 * (size_t)C * RP + 16) * 4 : (size_t)C * RP * 2));
   const size_t o_err = carve(sizeof(uint32_t));
   const size_t o_scal = carve(n * sizeof(uint4));
   const size_t o_ret = carve(n * sizeof(double));
@@ -3289,6 +3446,20 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
   const size_t o_vpend = carve(n * sizeof(uint32_t));
   const size_t o_expl = carve(n * (size_t)g.estride * 4);
   h->bytes = off;
+  if (is_far(h->variant)) {
+    // pe_step_far loads a quadrant's off-map rows UNCLAMPED (pe_far.hpp far_sector: up to
+    // R rows before the env's grid block and R rows + one raw word after it, selected away
+    // afterwards): the first env's must land in the arrays carved before the grid, the last
+    // env's in those after it -- inside this one allocation
+    const size_t row_b = (size_t)kFarRow32 * 4, grid_end = o_grid + n * (size_t)g.gstride * 8;
+    if (g.WPR != kCoopWPR || o_grid < (size_t)R * row_b || h->bytes - grid_end < (size_t)(R + 1) * row_b) {
+      delete[] ldx;
+      delete[] ldy;
+      delete h;
+      return fail(PE_ERR_ARG, "pe_step_far: the allocation leaves less than R padded grid rows of slack around the "
+                              "grid array (its off-map row loads would leave the allocation)");
+    }
+  }
   hipError_t me = hipMalloc(&h->mem, h->bytes);
   if (me != hipSuccess) {
     delete[] ldx;
@@ -3366,11 +3537,35 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
     e5 = hipMemcpy(base + o_ldxy, aln.data(), aln.size(), hipMemcpyHostToDevice);
   } else if (rt_tab) {  // the runtime sector kernel's entries (pe_quad.hpp quad_rays_rt): the probe's LDS
                         // byte offset from the rover row (dx rows of 64 envs x 8 B) | its bit shift 2(dy+R) << 16
-    std::vector<uint32_t> rt((size_t)C * RP, 0u);
+    std::vector<uint32_t> rt(2 * (size_t)C * RP + 16, 0u);
     for (int i = 0; i < C; ++i)
       for (int r = 0; r < R; ++r)
         rt[(size_t)i * RP + r] = (uint32_t)(uint16_t)(int16_t)(ldx[i * R + r] * kQuadEnvs * 8) |
                                  ((uint32_t)(2 * (ldy[i * R + r] + R)) << 16);
+    // the register-window form (pe_quad.hpp quad_rays_rt_reg): per wave w (rays [wC/4, (w+1)C/4))
+    // the header {LO, DLO, NROWS, ok}, per probe (dx - LO) | 2(dy - DLO) << 8
+    uint32_t* hdr = rt.data() + (size_t)C * RP;
+    uint32_t* ent = hdr + 16;
+    for (int w = 0; w < 4; ++w) {
+      const int i0 = w * C / 4, i1 = (w + 1) * C / 4;
+      int lo = 1 << 20, hi = -(1 << 20), dlo = 1 << 20, dhi = -(1 << 20);
+      for (int i = i0; i < i1; ++i)
+        for (int r = 0; r < R; ++r) {
+          lo = std::min(lo, (int)ldx[i * R + r]);
+          hi = std::max(hi, (int)ldx[i * R + r]);
+          dlo = std::min(dlo, (int)ldy[i * R + r]);
+          dhi = std::max(dhi, (int)ldy[i * R + r]);
+        }
+      const bool ok = i1 > i0 && hi - lo + 1 <= kRtRegRows && dhi - dlo + 1 <= 16;
+      hdr[4 * w] = (uint32_t)lo;
+      hdr[4 * w + 1] = (uint32_t)dlo;
+      hdr[4 * w + 2] = (uint32_t)(hi - lo + 1);
+      hdr[4 * w + 3] = ok ? 1u : 0u;
+      if (ok)
+        for (int i = i0; i < i1; ++i)
+          for (int r = 0; r < R; ++r)
+            ent[(size_t)i * RP + r] = (uint32_t)(ldx[i * R + r] - lo) | ((uint32_t)(2 * (ldy[i * R + r] - dlo)) << 8);
+    }
     e5 = hipMemcpy(base + o_ldxy, rt.data(), rt.size() * 4, hipMemcpyHostToDevice);
   } else {
     e5 = hipMemcpy(base + o_ldxy, ldxy.data(), ldxy.size() * 2, hipMemcpyHostToDevice);

@@ -72,8 +72,11 @@ def run(argv):
     done = (te.bool() | tr.bool()).cpu().numpy()
     L = _capi.lib()
     L.pe_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
-    NWQ = int(os.environ.get("PE_QUAD_WAVES", "4"))
-    nw = (n + 63) // 64 * NWQ
+    # envs per workgroup and waves per workgroup of the stamped kernel (the small-batch shapes:
+    # E16 with 8 waves at <= 4096 envs, E16 / E32 with 4 waves up to 32768; --epb / --waves)
+    EPB = arg("--epb", 64)
+    NWQ = arg("--waves", int(os.environ.get("PE_QUAD_WAVES", "4")))
+    nw = (n + EPB - 1) // EPB * NWQ
     buf = np.zeros(nw * 8, np.uint64)
     _capi.check(L.pe_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.size), "stamps")
     st = buf.reshape(nw, 8).astype(np.int64)
@@ -87,8 +90,8 @@ def run(argv):
                                                          "p90": int(np.percentile(rel[:, k] - rel[:, k - 1], 90))}
                         for k in range(1, 8)}}
     if desync:
-        nb = (n + 63) // 64
-        dpb = np.add.reduceat(done.astype(np.int64), np.arange(0, n, 64))
+        nb = (n + EPB - 1) // EPB
+        dpb = np.add.reduceat(done.astype(np.int64), np.arange(0, n, EPB))
         L.pe_debug_dstamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
         dbuf = np.zeros(nb * 8, np.uint64)
         _capi.check(L.pe_debug_dstamps(dbuf.ctypes.data_as(ctypes.c_void_p), dbuf.size), "dstamps")
