@@ -35,6 +35,9 @@
 #pragma once
 
 constexpr int kFarWaves = 4;
+#ifndef PE_FAR_INFO_REG
+#define PE_FAR_INFO_REG 0  // the terminal-info rows register-staged by the info wave (round 6 A/B: slower)
+#endif
 #ifndef PE_FAR_ROW_BATCH
 #define PE_FAR_ROW_BATCH 33  // one batch: the compiler's schedule (9: 55.1 us, 12: 54.3, 17: 54.6, 33: 53.7 at
                              // 64x64/C64/R32, same box, profiles/r5f/, r5h/)
@@ -114,7 +117,8 @@ __host__ __device__ constexpr int far_info_park_unit(int G, int WPR, int C) {
 }
 __host__ __device__ constexpr int far_lds_floats(int G, int WPR, int C, int R) {
   // (whole 64-unit LDS-DMA instructions: every lane of the last one writes its unit)
-  return far_stage_off(G, WPR, C, R) + 4 * 64 * ((far_info_park_unit(G, WPR, C) + 2 + 63) / 64);
+  return far_stage_off(G, WPR, C, R) +
+         4 * 64 * (((PE_FAR_INFO_REG ? far_info_park_unit(G, WPR, C) + 2 : far_stage_units(G, WPR, C)) + 63) / 64);
 }
 
 // Quadrant W's rays for this lane's env at the post-move position (xp, yp): first hit
@@ -313,13 +317,24 @@ __device__ __forceinline__ bool far_commit(const StepArgs& a, int64_t e, Scal& s
 template <int C, int R>
 __device__ __attribute__((noinline)) uint4 far_done(const void* ka, int tile_off, int lane, int wv, int64_t e0,
                                                     bool done, uint4 sp, double ret, int ndone, bool wfix,
-                                                    const float* ctab, const float* stage, bool stage_info,
-                                                    bool info_iw, int park_unit) {
+                                                    const float* ctab, const float* stage, bool stage_info) {
+  constexpr int D = 5 * C + 27;
+  return quad_done_path<kFarWaves, false, (D + 63) / 64, true>(ka, tile_off, C, R, lane, wv, kFarWaves - 1, e0, done,
+                                                               sp, ret, ndone, wfix, ctab, stage, stage_info);
+}
+#if PE_FAR_INFO_REG
+// (the A/B form: the info wave writes the terminal info from the rows it staged)
+template <int C, int R>
+__device__ __attribute__((noinline)) uint4 far_done_iw(const void* ka, int tile_off, int lane, int wv, int64_t e0,
+                                                       bool done, uint4 sp, double ret, int ndone, bool wfix,
+                                                       const float* ctab, const float* stage, bool stage_info,
+                                                       bool info_iw, int park_unit) {
   constexpr int D = 5 * C + 27;
   return quad_done_path<kFarWaves, false, (D + 63) / 64, true>(
       ka, tile_off, C, R, lane, wv, kFarWaves - 1, e0, done, sp, ret, ndone, wfix, ctab, stage, stage_info, -1,
       nullptr, nullptr, -1, false, info_iw, stage ? stage + 4 * park_unit : nullptr);
 }
+#endif
 
 template <int C, int R>
 __global__ __launch_bounds__(64 * kFarWaves, 4) void pe_step_far(StepArgs a) {
@@ -389,7 +404,9 @@ __global__ __launch_bounds__(64 * kFarWaves, 4) void pe_step_far(StepArgs a) {
   // wave then writes the terminal info beside the commit wave's reset, instead of the commit
   // wave loading the rows after the done barrier (a round trip on the one-done block's path)
   const int ng_s = pf_grid_units(g.G, g.WPR);
-  const bool info_reg = PE_BT_INFO_REG && stage_ok && !st.cur && a.tinfo != nullptr && ng_s <= 128;
+  // (measured slower here: 64x64/C64/R32 desync 60.0 -> 61.0 us, sync 52.8 -> 53.2, profiles/r6e/ --
+  // the kernel is at its register cap; A/B: -DPE_FAR_INFO_REG=1)
+  const bool info_reg = PE_FAR_INFO_REG && stage_ok && !st.cur && a.tinfo != nullptr && ng_s <= 128;
   uint4 iq0 = make_uint4(0u, 0u, 0u, 0u), iq1 = iq0;
   if (stage_ok) {
     const uint64_t pm = __ballot(s.step + 1 >= a.rl.max_steps);
@@ -525,8 +542,13 @@ __global__ __launch_bounds__(64 * kFarWaves, 4) void pe_step_far(StepArgs a) {
       rv = __hiloint2double((int)park[320 + lane], (int)park[256 + lane]);
     }
     const bool staged = stage_ok && npred == 1 && ndone == 1;  // then the done env is the predicted one
+#if PE_FAR_INFO_REG
+    sp = far_done_iw<C, R>(kernargs(), tile_off, lane, wv, e0, done, sp, rv, ndone, wfix, ctab, staged ? stage : nullptr,
+                           staged && stage_info, staged && info_reg, park_unit);
+#else
     sp = far_done<C, R>(kernargs(), tile_off, lane, wv, e0, done, sp, rv, ndone, wfix, ctab, staged ? stage : nullptr,
-                        staged && stage_info, staged && info_reg, park_unit);
+                        staged && stage_info);
+#endif
   }
   if (wv == CW) __builtin_amdgcn_s_waitcnt(0x0F70);  // tracked vmcnt(0): no wait inside the store loop
 #if defined(PE_FAR_PROBE) && PE_FAR_PROBE == 2  // timing probe (no obs): no tile store

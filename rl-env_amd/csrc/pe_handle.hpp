@@ -23,6 +23,7 @@ struct pe_handle {
   size_t lds_floor;  // minimum dynamic LDS per step workgroup (PE_LDS_FLOOR, debug builds only)
   int quad_waves;    // waves per workgroup of the sector kernel (4; 8 via PE_QUAD_WAVES in debug builds)
   int quad_epb;      // envs per workgroup of the sector kernel (64; 16 / 32 for small batches, C16R6 one-word)
+  int gr2;           // the two-word C16R6 kernel with the grid block in round 1 (pe_step_quad GR2)
   int stagger;       // sector-kernel start delay per block quarter (PE_STAGGER, debug builds only)
   int pipe_wpc;      // > 0: the persistent pipelined sector kernel (pe_step_pipe), this many
                      // workgroups per CU; 0: pe_step_quad

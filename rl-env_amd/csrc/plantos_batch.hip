@@ -540,14 +540,23 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
 #define PE_BT_EARLY 1  // the byte-coded one-word kernel loads a predicted single truncation's record early (A/B: 0)
 #endif
 #ifndef PE_REG_STAGE
-#define PE_REG_STAGE 1  // f32 kernels without the early record: a predicted single truncation's record
-                        // register-staged into LDS during round 2 (A/B: 0)
+#define PE_REG_STAGE 0  // f32 kernels without the early record: a predicted single truncation's record
+                        // register-staged into LDS during round 2 (round 6 A/B: not kept)
 #endif
 #ifndef PE_RT_REG
 #define PE_RT_REG 1  // runtime sector kernel: rays from a per-wave register window (A/B: 0, the LDS-table form)
 #endif
 #ifndef PE_BT_INFO_REG
 #define PE_BT_INFO_REG 1  // byte-coded LDS-DMA kernels: the info rows register-staged by the info wave (A/B: 0)
+#endif
+#ifndef PE_GR2
+#define PE_GR2 0  // the two-word C16R6 kernel (G <= 28) loads the loader env's grid block in round 1 (A/B: not kept)
+#endif
+#ifndef PE_EARLY2
+#define PE_EARLY2 0  // one-word early-record kernels: two predicted truncations' records by waves 0 and 1 (A/B: not kept)
+#endif
+#ifndef PE_REG_STAGE_SMALL
+#define PE_REG_STAGE_SMALL 0  // ... and the 16 / 32-env small-batch shapes (A/B: 1)
 #endif
 #ifndef PE_BT_STAGE_MIN_C
 #define PE_BT_STAGE_MIN_C 64  // byte-coded kernels stage the predicted record by LDS-DMA from this C on (A/B: 0)
@@ -900,9 +909,11 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         PfLoad<MAXW, KD> pl;
         if (a.pf.scal && !eh) coop_load_prefetched<MAXW, KD, OT>(a.pf, g, el, pl, lane);
         if (a.tinfo) {
-          if (eh && !kIW)
+          // (with the info wave the single early env's rows are that wave's, not this one's;
+          // kEarly2's waves hold their env's rows themselves: e_info == e_early)
+          if (eh && (!kIW || e_info == el))
             coop_info_store<MAXW>(st, g, *early_rows, sv, a.tinfo + el * PE_NINFO, lane, kw >> 1, ltab);
-          else  // (with the info wave the early rows are that wave's, not this one's)
+          else
             coop_write_info<MAXW>(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, kw >> 1, ltab);
         }
         Row4<MAXW> rw;
@@ -1271,7 +1282,11 @@ __device__ __forceinline__ void quad_compute(const StepArgs& a, const uint64_t* 
 // EPB: envs per workgroup (64; 16 / 32 for small batches: more workgroups, so that
 // a batch of a few thousand envs spreads over every CU -- lanes >= EPB idle).  The
 // LDS layout keeps the 64-env stride LS whatever EPB.
-template <int C, int R, bool ONEWORD, int NW, bool BT = false, int EPB = kQuadEnvs>
+// GR2 (round 6): two-word rows (WPR == 2) of a grid small enough (G <= kGr2MaxG: 25x25, the
+// training scripts' grid) that the loader env's whole block comes in round 1, as the one-word
+// kernel's (kGridR1): round 2 then holds only the visit rows.
+constexpr int kGr2MaxG = 28;
+template <int C, int R, bool ONEWORD, int NW, bool BT = false, int EPB = kQuadEnvs, bool GR2 = false>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) void pe_step_quad(StepArgs a) {  // NW=8: <= 80 SGPRs (small-batch EPB: one workgroup per CU, no cap); NW=4: <= 128 VGPRs (4 workgroups per CU: G=25 13.1 -> 10.5 us; 1-word C16: 122 -> 104 VGPRs)
   // C == 0 (R == 0): the runtime-(C, R) sector kernel (quad_rays_rt): C, R from the
   // geometry (up to kRtCMax -- kRtCMaxBT with the byte-coded tile -- / kRtRMax), the LDS
@@ -1346,8 +1361,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // one-word rows (G <= 20): the loader env's whole grid block (gstride / 2 <= 10
   // 16-B units, contiguous, 3 per loader thread) comes in round 1 -- its address does
   // not depend on the position -- and only the visit rows are left for round 2
-  constexpr int JG1 = (10 + LT - 1) / LT;  // gstride / 2 <= 10 16-B units (one-word: NW == 4, G <= 20)
-  constexpr bool kGridR1 = ONEWORD && PE_GRID_R1;
+  static_assert(!GR2 || (!ONEWORD && !RT && NW == 4 && EPB == kQuadEnvs), "GR2: the two-word 64-env kernel");
+  constexpr int JG1 = GR2 ? (kGr2MaxG + LT - 1) / LT : (10 + LT - 1) / LT;  // gstride / 2 <= 10 16-B units (one-word:
+                                                                            // NW == 4, G <= 20); GR2: G <= kGr2MaxG rows
+  constexpr bool kGridR1 = (ONEWORD && PE_GRID_R1) || GR2;
   uint4 qg1[kGridR1 ? JG1 : 1];
   if constexpr (kGridR1) {
     const uint4* lgq = reinterpret_cast<const uint4*>(st.grid + elc * g.gstride);
@@ -1450,12 +1467,25 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
     // predicted env per wave took the desynchronized step 11.16 -> 11.06 us but the
     // synchronized one 9.42 -> 9.49, profiles/r3g_ab_*.jsonl; round 5: the env's rows
     // for its terminal info by the info wave)
-    if ((wv == CW || (kInfoW && wv == kQuadInfoWave)) && a.pf.scal && a.autoreset && !st.cur) {
+    // (round 6, kEarly2: a block with exactly TWO predicted truncations -- ~2 of the 1024
+    // blocks of a desynchronized 65536-env step, which the one-done blocks' early record left
+    // as the step's last blocks -- has waves 0 and 1 load one env's record and rows each:
+    // the cooperative path hands the k-th done env to wave k, so each finds its own)
+    constexpr bool kEarly2 = PE_EARLY2 && NW == 4;
+    if ((wv == CW || (kInfoW && wv == kQuadInfoWave) || (kEarly2 && wv < 2)) && a.pf.scal && a.autoreset && !st.cur) {
       const uint64_t pmk = __ballot(live && s.step + 1 >= rl.max_steps);
       const uint32_t plo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pmk),
                      phi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pmk >> 32));
       const uint64_t pmu = (uint64_t)plo | ((uint64_t)phi << 32);
-      if (__popcll(pmu) == 1) {
+      const int npk = __popcll(pmu);
+      if (kEarly2 && npk == 2 && wv < 2) {
+        const uint64_t lowb = pmu & (0ull - pmu);
+        const int64_t ep = e0 + (__ffsll((unsigned long long)(wv == 0 ? lowb : (pmu ^ lowb))) - 1);
+        e_early = ep;
+        e_info = ep;
+        coop_load_prefetched<MAXWQ, KDQ, OT>(a.pf, g, ep, epl, lane);
+        eir = coop_info_rows<MAXWQ>(st, g, ep, lane);
+      } else if (npk == 1 && wv >= 2) {
         const int64_t ep = e0 + (__ffsll((unsigned long long)pmu) - 1);
         if (wv == CW) {
           e_early = ep;
@@ -1481,7 +1511,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // info wave writes the terminal info from the staged rows beside it.
   // (not the 16 / 32-env small-batch shapes: 4096 envs synchronized 4.43 -> 4.62 us for
   // desynchronized 6.38 -> 6.30, profiles/r6c/)
-  constexpr bool kRegStage = PE_REG_STAGE && !kEarlyRec && !BT && NW > kQuadInfoWave && EPB == kQuadEnvs;
+  constexpr bool kRegStage =
+      PE_REG_STAGE && !kEarlyRec && !BT && NW > kQuadInfoWave && (EPB == kQuadEnvs || PE_REG_STAGE_SMALL);
   // (the staging outcome goes to LDS -- kRsFlagF, written by the commit wave every launch --
   // and the done env's scalars are parked after the compute phase: no SGPRs live across it)
   constexpr int kRsFlagF = kInfoParkF + 5;
@@ -1611,10 +1642,12 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
       const int lyb = ly > 0 ? ly - 1 : 0;
       const int w0 = (2 * lyb) >> 6, o = (2 * lyb) & 63;
       const int w1 = w0 + 1 < g.WPR ? w0 + 1 : w0;  // in bounds; its word is dropped when w0 is the last
-      constexpr int JG = (NR + LT - 1) / LT, JV = (NV + LT - 1) / LT;
+      constexpr int JG = GR2 ? 1 : (NR + LT - 1) / LT, JV = (NV + LT - 1) / LT;
       uint64_t glo[JG], ghi[JG];
       uint32_t vlo[JV], vhi[JV];
-      if (g.WPR == 2) {  // (G <= 52, e.g. the training scripts' 25x25) a row is one aligned 16-B load
+      if constexpr (GR2) {
+        // (the rows came with round 1: qg1, unit q = grid row q)
+      } else if (g.WPR == 2) {  // (G <= 52, e.g. the training scripts' 25x25) a row is one aligned 16-B load
 #pragma unroll
         for (int j = 0; j < JG; ++j) {
           const int xr = base + sub + LT * j;
@@ -1646,10 +1679,29 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
       }
       stage_issue();
       rs_issue();  // (after round 2's loads: their waits stay as they were)
+      if constexpr (GR2) {
+        // the loader env's rows inside the window, funnel-shifted to padded column yb, then
+        // the off-map rows (obstacles)
+#pragma unroll
+        for (int j = 0; j < JG1; ++j) {
+          const int q = sub + LT * j, k = q - base;
+          if (q < g.G && k >= 0 && k < NRL) {
+            const uint64_t lo64 = (uint64_t)qg1[j].x | ((uint64_t)qg1[j].y << 32);
+            const uint64_t hi64 = (uint64_t)qg1[j].z | ((uint64_t)qg1[j].w << 32);
+            const uint64_t lo = w0 ? hi64 : lo64, hi = w0 ? 0ull : hi64;
+            lrow[k * LS + le] = o ? ((lo >> o) | (hi << (64 - o))) : lo;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < (NR + LT - 1) / LT; ++j) {
+          const int k = sub + LT * j, xr = base + k;
+          if (k < NRL && (xr < 0 || xr >= g.G)) lrow[k * LS + le] = kEven64;  // off-map rows: obstacles
+        }
+      }
 #pragma unroll
       for (int j = 0; j < JG; ++j) {
         const int k = sub + LT * j;
-        if (k < NRL) {
+        if (!GR2 && k < NRL) {
           const int xr = base + k;
           uint64_t v = kEven64;  // off-map rows read as obstacles
           if (xr >= 0 && xr < g.G) {
@@ -1703,7 +1755,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? (EPB < kQuadEnvs ? 2 : 8) : 4) v
   // (not asm), so that the done path's first use of it carries none -- otherwise it
   // waits vmcnt(0) there, i.e. for the commit's stores too (in-order counter)
   if constexpr (kEarlyRec) {
-    if (wv == CW || (kInfoW && wv == kQuadInfoWave)) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    if (wv == CW || (kInfoW && wv == kQuadInfoWave) || (PE_EARLY2 && NW == 4 && wv < 2))
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   }
   PE_STAMP(2);
   __syncthreads();
@@ -2973,7 +3026,14 @@ int launch_step(const pe_handle* h, const StepArgs& a, hipStream_t s) {
         else
           PE_QUAD(16, 6, true);
         break;
-      case V_QUAD_C16R6: PE_QUAD4(16, 6, false); break;
+      case V_QUAD_C16R6:
+#if PE_GR2
+        if (h->gr2)
+          hipLaunchKernelGGL((pe_step_quad<16, 6, false, 4, false, kQuadEnvs, true>), grid, block, lds, s, a);
+        else
+#endif
+          PE_QUAD4(16, 6, false);
+        break;
 #ifdef PE_DEBUG_KNOBS
       case V_QUAD_C64R6: PE_QUAD(64, 6, false); break;  // (PE_TILE_CODES=0: the f32-tile A/B)
 #else
@@ -3350,7 +3410,8 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
     // would run their load, compute and 89-KB store phases in lockstep: starting the
     // grid's quarters ~0.85 us apart overlaps one quarter's stores with the next
     // one's loads (64x64 / 64 rays, same-box: 28.7 -> 26.3 us; 2x that: 27.0)
-    h->stagger = h->variant == V_QUAD_C16R6_1W ? 0 : 4;
+    // (the far kernel: 8 -- 52.8 -> 52.1 us, desynchronized unchanged, profiles/r6d/ab_farstag)
+    h->stagger = h->variant == V_QUAD_C16R6_1W ? 0 : (is_far(h->variant) ? 8 : 4);
   }
 #ifdef PE_DEBUG_KNOBS
   if (const char* sg = std::getenv("PE_STAGGER")) h->stagger = std::atoi(sg);
@@ -3409,6 +3470,10 @@ int pe_create(const pe_config* c, int32_t device, int32_t n_envs, pe_handle** ou
     std::snprintf(h->kname_buf, sizeof(h->kname_buf), "%.*s,bytetile>", (int)std::strlen(h->kname) - 1, h->kname);
     h->kname = h->kname_buf;
   }
+  // the two-word kernel with the loader env's whole grid block in round 1 (pe_step_quad GR2)
+  h->gr2 = PE_GR2 && h->variant == V_QUAD_C16R6 && g.WPR == 2 && G <= kGr2MaxG && !h->tile_codes &&
+           h->quad_waves == 4 && h->quad_epb == kQuadEnvs;
+  if (h->gr2) h->kname = "pe_step_quad<C16,R6,gridr1>";
   // explicit reset-path tuning (pe_config.coop_max_done; -1: the choice above) --
   // applied before the prefetch decision, which depends on it
   if (c->coop_max_done >= 0 && coop_reset_ok(G, R, g.WPR, g.NW, P, C, c->map_generation_algo))

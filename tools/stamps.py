@@ -108,6 +108,9 @@ def run(argv):
             "block_end_no_done_p50": int(np.median(rel.reshape(nb, NWQ, 8)[none, :, 7].max(1))),
             "block_end_one_done_p50": int(np.median(rel.reshape(nb, NWQ, 8)[one, :, 7].max(1))),
             "block_end_one_done_p90": int(np.percentile(rel.reshape(nb, NWQ, 8)[one, :, 7].max(1), 90)),
+            # the last block of each done count (the step ends with the slowest block)
+            "block_end_max_by_done": {int(k): int(rel.reshape(nb, NWQ, 8)[dpb == k, :, 7].max())
+                                      for k in np.unique(dpb)},
             "done_points": "single-done path (commit wave): d0 entry, d1 tobs copied, d2 info written, "
                            "d3 reset taken+applied, d4 queue flag, d5 scalars stored"}
     print(json.dumps(out))

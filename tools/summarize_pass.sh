@@ -45,4 +45,14 @@ for x in g64r32 g40c48 g32; do
   python3 tools/pmc_summary.py $T --out-prefix pmc_$x --fetch-dir pmcx_${x}_FETCH_SIZE_$T \
     --write-dir pmcx_${x}_WRITE_SIZE_$T --bench-json $G/pmcx_${x}_FETCH_SIZE_$T.json --stats-dir statsx_${x}_$T > /dev/null
 done
+# the root's 8-block expansion of config 5 (bench.py gather leg expand_w8_us), from the gather trace
+python3 tools/expand_w8_summary.py $G/statsx_gather_$T/run_kernel_trace.csv $P/${T}_expand_w8_trace.csv \
+  $P/${T}_expand_w8.json $G/statsx_gather_$T.json
+# the desynchronized steady state of every geometry (tools/measure_desync.sh): step + prefetch + compaction
+for x in head n4096 g25 g21 g15 g64 g64r32 g32 g40c48; do
+  d=$G/statsx_d${x}_$T
+  [ -f $d/run_kernel_stats.csv ] || continue
+  cp $d/run_kernel_stats.csv $P/${T}_kernel_stats_desync_$x.csv
+  python3 tools/desync_summary.py $P/kstats_${T}_desync_$x.json $P/${T}_kernel_stats_desync_$x.csv $G/statsx_d${x}_$T.json
+done
 ls -la $P/*_$T.json $P/${T}_* | wc -l
