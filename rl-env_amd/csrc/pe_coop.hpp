@@ -897,8 +897,9 @@ __device__ __forceinline__ Row4<MAXW> pf_stage_rows(const uint64_t* w, const Geo
   return r;
 }
 
-// coop_take_prefetched from the staged record (after the wave's vmcnt(0)).
-template <int MAXW, typename OT>
+// coop_take_prefetched from the staged record (after the wave's vmcnt(0)).  KD > 0: the obs
+// row (at most 64 * KD values) copied as batched reads, then writes.
+template <int MAXW, typename OT, int KD = 0>
 __device__ __forceinline__ bool pf_stage_take(const float* lds, const Geo& g, int ostride, uint32_t episode,
                                               Row4<MAXW>& rw, Scal& s, OT* out, int lane) {
   const uint4 ps = *reinterpret_cast<const uint4*>(lds);
@@ -910,7 +911,16 @@ __device__ __forceinline__ bool pf_stage_take(const float* lds, const Geo& g, in
   const int ng = pf_grid_units(g.G, g.WPR);
   rw = pf_stage_rows<MAXW>(reinterpret_cast<const uint64_t*>(lds + 4), g, lane);
   const OT* o = reinterpret_cast<const OT*>(lds + 4 + 4 * ng);
-  for (int k = lane; k < g.D; k += 64) out[k] = o[k];
+  if constexpr (KD > 0) {
+    OT v[KD];
+#pragma unroll
+    for (int j = 0; j < KD; ++j) v[j] = lane + 64 * j < g.D ? o[lane + 64 * j] : OT(0);
+#pragma unroll
+    for (int j = 0; j < KD; ++j)
+      if (lane + 64 * j < g.D) out[lane + 64 * j] = v[j];
+  } else {
+    for (int k = lane; k < g.D; k += 64) out[k] = o[k];
+  }
   (void)ostride;
   return true;
 }

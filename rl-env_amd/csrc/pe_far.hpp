@@ -319,8 +319,8 @@ __device__ __attribute__((noinline)) uint4 far_done(const void* ka, int tile_off
                                                     bool done, uint4 sp, double ret, int ndone, bool wfix,
                                                     const float* ctab, const float* stage, bool stage_info) {
   constexpr int D = 5 * C + 27;
-  return quad_done_path<kFarWaves, false, (D + 63) / 64, true>(ka, tile_off, C, R, lane, wv, kFarWaves - 1, e0, done,
-                                                               sp, ret, ndone, wfix, ctab, stage, stage_info);
+  return quad_done_path<kFarWaves, false, (D + 63) / 64, true, true>(ka, tile_off, C, R, lane, wv, kFarWaves - 1, e0,
+                                                                     done, sp, ret, ndone, wfix, ctab, stage, stage_info);
 }
 #if PE_FAR_INFO_REG
 // (the A/B form: the info wave writes the terminal info from the rows it staged)

@@ -558,6 +558,9 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
 #ifndef PE_REG_STAGE_SMALL
 #define PE_REG_STAGE_SMALL 0  // ... and the 16 / 32-env small-batch shapes (A/B: 1)
 #endif
+#ifndef PE_DONE_BATCH
+#define PE_DONE_BATCH 1  // done path: the terminal / fresh obs row copies as batched reads, then writes (A/B: 0)
+#endif
 #ifndef PE_BT_STAGE_MIN_C
 #define PE_BT_STAGE_MIN_C 64  // byte-coded kernels stage the predicted record by LDS-DMA from this C on (A/B: 0)
 #endif
@@ -673,7 +676,11 @@ __device__ __forceinline__ bool el_info_hit(int64_t e_info, int64_t e0, const fl
 }
 
 // BT: the obs tile holds byte codes (ctab: the LDS code table), see pe_step_quad.
-template <int NW, bool ONEWORD, int KD, bool BT = false>  // one copy per kernel: each inherits its kernel's register budget
+// DB: the row copies batched (PE_DONE_BATCH) -- where the registers are there: rows of at most
+// 128 values, or a path out of line (the far kernel's far_done); inlined into the C64 / runtime
+// byte-tile kernels (KD = 6) it cost their hot path (64x64/C64 24.15 -> 25.0 us, profiles/r6h/)
+template <int NW, bool ONEWORD, int KD, bool BT = false, bool DB = (KD <= 2)>  // one copy per kernel: each
+                                                                              // inherits its kernel's register budget
 __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, int C, int R, int lane, int wv, int CW,
                                                 int64_t e0, bool done, uint4 sp, double ret, int ndone, bool wfix,
                                                 const float* ctab = nullptr, const float* stage = nullptr,
@@ -778,9 +785,18 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
                                           (uint32_t)__builtin_amdgcn_readlane((int)sp.y, l),
                                           (uint32_t)__builtin_amdgcn_readlane((int)sp.z, l),
                                           (uint32_t)__builtin_amdgcn_readlane((int)sp.w, l)));
-        if (a.tobs) {
+        if (a.tobs) {  // (the row's reads first, then the stores: one LDS round trip, not one per 64 values)
           float* t = a.tobs + el * g.D;
-          for (int k2 = lane; k2 < g.D; k2 += 64) t[k2] = tval(orow, k2);
+          if constexpr (PE_DONE_BATCH && DB) {
+            float tv[KD];
+#pragma unroll
+            for (int j = 0; j < KD; ++j) tv[j] = lane + 64 * j < g.D ? tval(orow, lane + 64 * j) : 0.0f;
+#pragma unroll
+            for (int j = 0; j < KD; ++j)
+              if (lane + 64 * j < g.D) t[lane + 64 * j] = tv[j];
+          } else {
+            for (int k2 = lane; k2 < g.D; k2 += 64) t[k2] = tval(orow, k2);
+          }
         }
         // with the curriculum the commit stored this env's rows: they must land before
         // the info reads them and the reset rewrites them
@@ -800,7 +816,8 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         Row4<MAXW> rw;
         Scal ns;
         asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
-        const bool took = stage ? pf_stage_take<MAXW>(stage, g, (int)a.pf.ostride, sv.episode, rw, ns, orow, lane)
+        const bool took = stage ? pf_stage_take<MAXW, OT, PE_DONE_BATCH && DB ? KD : 0>(stage, g, (int)a.pf.ostride, sv.episode,
+                                                                                  rw, ns, orow, lane)
                                 : (a.pf.scal && take(el, sv.episode, pl, rw, ns, orow));
         if (took) {
           ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane, ltab, true);
@@ -892,9 +909,18 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         if (k % NWv != wv) continue;
         const int64_t el = e0 + l;
         OT* orow = rows + l * g.D;
-        if (a.tobs) {
+        if (a.tobs) {  // (the row's reads first, then the stores: one LDS round trip, not one per 64 values)
           float* t = a.tobs + el * g.D;
-          for (int k2 = lane; k2 < g.D; k2 += 64) t[k2] = tval(orow, k2);
+          if constexpr (PE_DONE_BATCH && DB) {
+            float tv[KD];
+#pragma unroll
+            for (int j = 0; j < KD; ++j) tv[j] = lane + 64 * j < g.D ? tval(orow, lane + 64 * j) : 0.0f;
+#pragma unroll
+            for (int j = 0; j < KD; ++j)
+              if (lane + 64 * j < g.D) t[lane + 64 * j] = tv[j];
+          } else {
+            for (int k2 = lane; k2 < g.D; k2 += 64) t[k2] = tval(orow, k2);
+          }
         }
         const uint4 sl = make_uint4((uint32_t)__builtin_amdgcn_readfirstlane((int)stage[5 * l]),
                                     (uint32_t)__builtin_amdgcn_readfirstlane((int)stage[5 * l + 1]),
