@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The root's 8-block expansion (bench.py gather leg, expand_w8_us) from a rocprofv3
---kernel-trace run of bench.py: the pe_expand_codes_kernel dispatches whose grid is the
-8-block one (the largest Grid_Size_X of that kernel), their average duration, beside the
+--kernel-trace run of bench.py: the pe_expand_codes_kernel dispatches of the 8-block
+expansion (told apart by duration: more than 4x the short launches), their average duration, beside the
 1-block expansion and the codes step of the same run.  Writes the rows it used as a CSV
 and one JSON record.
   python tools/expand_w8_summary.py run_kernel_trace.csv OUT.csv OUT.json bench_line.json"""
@@ -14,10 +14,13 @@ def main():
     trace, out_csv, out_json, bench = sys.argv[1:5]
     rows = list(csv.DictReader(open(trace)))
     ex = [r for r in rows if "pe_expand_codes_kernel" in r["Kernel_Name"]]
-    gmax = max(int(r["Grid_Size_X"]) for r in ex)
-    gmin = min(int(r["Grid_Size_X"]) for r in ex)
-    w8 = [r for r in ex if int(r["Grid_Size_X"]) == gmax]
-    w1 = [r for r in ex if int(r["Grid_Size_X"]) == gmin]
+    # (the expansion kernel's grid does not grow with the blocks -- a grid-stride loop -- so the
+    # 8-block launches are told apart by duration: ~8x the 1-block ones)
+    d = lambda r: int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    lo = sorted(d(r) for r in ex)[len(ex) // 10]
+    w8 = [r for r in ex if d(r) > 4 * lo]
+    w1 = [r for r in ex if d(r) <= 4 * lo]
+    gmax = gmin = int(ex[0]["Grid_Size_X"])
     step = [r for r in rows if "pe_step_quad<16, 6, true, 4, true" in r["Kernel_Name"]]
     dur = lambda rr: sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rr) / max(1, len(rr)) / 1e3
     with open(out_csv, "w") as f:
