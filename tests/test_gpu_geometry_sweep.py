@@ -75,7 +75,13 @@ def _ids(geos):
     return [f"G{g}P{p}O{o}R{r}C{c}" for g, p, o, r, c in geos]
 
 
-@pytest.mark.parametrize("cfg", GEOS + WIDE + FAR, ids=_ids(GEOS) + _ids(WIDE) + _ids(FAR))
+# (round 6) runtime-sector geometries whose uneven compass sectors span more than 15 rows at
+# long range: those sectors take the LDS-table rays, the others the register window
+# (pe_quad.hpp quad_rays_rt_reg), in one launch -- C = 5 / 9 / 10 at R = 13 / 14
+MIXED = [(20, 8, 16, 14, 5), (23, 10, 20, 13, 9), (28, 12, 24, 14, 10)]
+
+
+@pytest.mark.parametrize("cfg", GEOS + WIDE + FAR + MIXED, ids=_ids(GEOS) + _ids(WIDE) + _ids(FAR) + _ids(MIXED))
 def test_geometry_sweep_parity(cfg):
     _sweep(cfg, codes=False)
 
