@@ -348,7 +348,12 @@ __device__ __forceinline__ void coop_merge(Row4<MAXW>& rw, uint64_t* scr, int WP
   }
 }
 
-template <int MAXW>
+// LT: `tab` is the caller's LDS copy of the tables, read as LDS.  (A generic pointer that may
+// hold it or st.tab turns every table read into a flat load, whose wait is vmcnt(0) as well:
+// behind every store the wave has in flight.)
+typedef const __attribute__((address_space(3))) Tables* LdsTables;
+
+template <int MAXW, bool LT = false>
 __device__ inline Scal coop_gen_map(const Geo& g, const Rules& rl, const Tables* tab, Row4<MAXW>& rw,
                                     uint32_t env_id, uint32_t episode, int lane, uint64_t* scr) {
   const int G = g.G, R = g.R;
@@ -357,8 +362,8 @@ __device__ inline Scal coop_gen_map(const Geo& g, const Rules& rl, const Tables*
 #pragma unroll
   for (int w = 0; w < MAXW; ++w) {
     const bool in = MAXW == 1 || w < g.WPR;
-    real[w] = in ? tab->grid_real[w] : 0ull;
-    rw.set(w, own && in ? tab->grid_pad[w] : 0ull);
+    real[w] = in ? (LT ? ((LdsTables)tab)->grid_real[w] : tab->grid_real[w]) : 0ull;
+    rw.set(w, own && in ? (LT ? ((LdsTables)tab)->grid_pad[w] : tab->grid_pad[w]) : 0ull);
   }
   PE_COOP_T(0);
   WaveStream rng;
@@ -536,7 +541,7 @@ __device__ __forceinline__ Row4<MAXW> coop_info_rows(const State& st, const Geo&
   return r;
 }
 
-template <int MAXW>
+template <int MAXW, bool LT = false>
 __device__ inline void coop_info_store(const State& st, const Geo& g, const Row4<MAXW>& rows, const Scal& s, int32_t* o,
                                        int lane, int wfix = 0, const Tables* tab = nullptr) {
   const Tables* T = tab ? tab : st.tab;  // the caller's LDS copy, if it has one
@@ -546,7 +551,8 @@ __device__ inline void coop_info_store(const State& st, const Geo& g, const Row4
     for (int w = 0; w < MAXW; ++w)
       if (MAXW == 1 || w < g.WPR) {
         const uint64_t v = rows.get(w);
-        const uint64_t lo = v & kEven64, hi = (v >> 1) & kEven64, real = T->grid_real[w];
+        const uint64_t lo = v & kEven64, hi = (v >> 1) & kEven64;
+        const uint64_t real = LT ? ((LdsTables)tab)->grid_real[w] : T->grid_real[w];
         th += __popcll(lo & hi & real);   // sum(plants.values())     :318
         hy += __popcll(~lo & hi & real);  // len(plants) - thirsty    :319
       }
@@ -571,10 +577,10 @@ __device__ inline void coop_info_store(const State& st, const Geo& g, const Row4
   if (lane < PE_NINFO) o[lane] = v;
 }
 
-template <int MAXW>
+template <int MAXW, bool LT = false>
 __device__ inline void coop_write_info(const State& st, const Geo& g, int64_t e, const Scal& s, int32_t* o, int lane,
                                        int wfix = 0, const Tables* tab = nullptr) {
-  coop_info_store<MAXW>(st, g, coop_info_rows<MAXW>(st, g, e, lane), s, o, lane, wfix, tab);
+  coop_info_store<MAXW, LT>(st, g, coop_info_rows<MAXW>(st, g, e, lane), s, o, lane, wfix, tab);
 }
 
 // Prefetched resets: the map of an env's NEXT reset depends only on (seed, env,
@@ -672,6 +678,7 @@ __device__ __forceinline__ bool coop_take_prefetched(const Prefetch& pf, const G
 // keep: CurriculumWrapper keeps the previous visit counts.
 // Fresh visit rows of a new episode (all zero, pads 10, visit[rover] = 1,
 // plantos_env.py:146-147) into its slot, lane r writing row r.
+template <bool LT = false>
 __device__ inline void coop_fresh_visits(const State& st, const Geo& g, int64_t e, const Scal& s, int lane,
                                          const Tables* tab) {
   if (lane < g.G) {
@@ -679,7 +686,7 @@ __device__ inline void coop_fresh_visits(const State& st, const Geo& g, int64_t 
     const int bit = 4 * (s.y + 2);
     const bool rover = lane == s.x && !(s.flags & F_NOROOM);
     for (int w = 0; w < g.NW; ++w) {
-      uint32_t v = (tab ? tab : st.tab)->vis_pad[w];
+      uint32_t v = LT ? ((LdsTables)tab)->vis_pad[w] : (tab ? tab : st.tab)->vis_pad[w];
       if (rover && w == (bit >> 5)) v = (v & ~(0xFu << (bit & 31))) | (1u << (bit & 31));
       vb[w] = v;
     }
@@ -688,7 +695,7 @@ __device__ inline void coop_fresh_visits(const State& st, const Geo& g, int64_t 
 
 // taken: s is a prefetched record's, whose fresh visit rows the prefetch kernel already
 // wrote into the new episode's slot (pe_device.hpp vis_env): no visit row is stored.
-template <int MAXW>
+template <int MAXW, bool LT = false>
 __device__ inline Scal coop_apply_reset(const State& st, const Geo& g, int64_t e, Scal s, bool keep,
                                         const Row4<MAXW>& rw, int lane,
                                         const Tables* tab = nullptr, bool taken = false) {
@@ -700,7 +707,7 @@ __device__ inline Scal coop_apply_reset(const State& st, const Geo& g, int64_t e
       if (MAXW == 1 || w < g.WPR) gb[w] = rw.get(w);
   }
   if (!keep && !taken) {  // reset_visits: all zero (pads 10), visit[rover] = 1 (:146-147)
-    coop_fresh_visits(st, g, e, s, lane, tab);
+    coop_fresh_visits<LT>(st, g, e, s, lane, tab);
   } else if (keep) {  // the previous episode's rows carried into the new slot, explored map restarted
     if (lane < g.G) {
       const uint32_t* src = vis_env(st, g, e, s.episode - 1u) + (int64_t)lane * g.NW;
@@ -717,12 +724,12 @@ __device__ inline Scal coop_apply_reset(const State& st, const Geo& g, int64_t e
 
 // reset() of env e (plantos_env.py:125-158) by one wave: map generation, then
 // coop_apply_reset.
-template <int MAXW>
+template <int MAXW, bool LT = false>
 __device__ inline Scal coop_reset_env(const State& st, const Geo& g, const Rules& rl, int64_t e, uint32_t episode,
                                       bool keep, Row4<MAXW>& rw, int lane, uint64_t* scr,
                                       const Tables* tab = nullptr) {
-  const Scal s = coop_gen_map<MAXW>(g, rl, tab ? tab : st.tab, rw, rl.env_off + (uint32_t)e, episode, lane, scr);
-  return coop_apply_reset<MAXW>(st, g, e, s, keep, rw, lane, tab);
+  const Scal s = coop_gen_map<MAXW, LT>(g, rl, LT ? tab : (tab ? tab : st.tab), rw, rl.env_off + (uint32_t)e, episode, lane, scr);
+  return coop_apply_reset<MAXW, LT>(st, g, e, s, keep, rw, lane, tab);
 }
 
 // Obs writers: an obs row of f32 values (HBM or an f32 LDS tile row), or of byte

@@ -561,6 +561,12 @@ __global__ __launch_bounds__(kBlock) void pe_step_fast(StepArgs a) {
 #ifndef PE_DONE_BATCH
 #define PE_DONE_BATCH 1  // done path: the terminal / fresh obs row copies as batched reads, then writes (A/B: 0)
 #endif
+#ifndef PE_DONE_ONEWAIT
+// done path without the early record: every load (record, terminal-info rows, terminal obs)
+// issued before any store, one wait, then the stores -- vmcnt counts stores too, in order, so
+// a load consumed after a store waits for that store (A/B: 0; 2: in every kernel)
+#define PE_DONE_ONEWAIT 1
+#endif
 #ifndef PE_BT_STAGE_MIN_C
 #define PE_BT_STAGE_MIN_C 64  // byte-coded kernels stage the predicted record by LDS-DMA from this C on (A/B: 0)
 #endif
@@ -711,6 +717,12 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
   constexpr int MAXW = ONEWORD ? 1 : kCoopWPR;
   // the early record's terminal info is the info wave's (the kernel's kInfoW)
   constexpr bool kIW = PE_INFO_WAVE && NW == 4 && ONEWORD && KD <= 2;
+  // loads before stores (PE_DONE_ONEWAIT): the one-word f32 kernels (1); every kernel with
+  // batched row copies (2: the multi-word and byte-tile ones measured slower)
+  constexpr bool kOneWait = PE_DONE_ONEWAIT && PE_DONE_BATCH && DB && (PE_DONE_ONEWAIT > 1 || (ONEWORD && !BT));
+  // the table reads of the reset / info helpers as LDS reads of ltab (pe_coop.hpp LdsTables):
+  // the one-word f32 kernels (the others measured slower with them, 64x64 +0.2 us desync)
+  constexpr bool kLT = ONEWORD && !BT;
   // an obs tile value as a float (BT: expand the code)
   auto tval = [&](const OT* r, int k) -> float {
     if constexpr (BT) return ctab[r[k]];
@@ -746,16 +758,16 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         for (int j = 0; j < KD; ++j) tv[j] = lane + 64 * j < g.D ? tval(orow, lane + 64 * j) : 0.0f;
         PE_DSTAMP(1);
         // (the terminal info: the info wave's, below, when it loaded the env's rows)
-        if (a.tinfo && !kIW) coop_info_store<MAXW>(st, g, *early_rows, sv, a.tinfo + el * PE_NINFO, lane, wf, ltab);
+        if (a.tinfo && !kIW) coop_info_store<MAXW, kLT>(st, g, *early_rows, sv, a.tinfo + el * PE_NINFO, lane, wf, ltab);
         PE_DSTAMP(2);
         Row4<MAXW> rw;
         Scal ns;
         asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
         if (take(el, sv.episode, *early, rw, ns, orow)) {
-          ns = coop_apply_reset<MAXW>(st, g, el, ns, false, rw, lane, ltab, true);
+          ns = coop_apply_reset<MAXW, kLT>(st, g, el, ns, false, rw, lane, ltab, true);
         } else {  // the record is not this reset's (not generated yet): generate in place
           uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
-          ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, false, rw, lane, scr, ltab);
+          ns = coop_reset_env<MAXW, kLT>(st, g, rl, el, sv.episode, false, rw, lane, scr, ltab);
           coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
         }
         PE_DSTAMP(3);
@@ -785,56 +797,108 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
                                           (uint32_t)__builtin_amdgcn_readlane((int)sp.y, l),
                                           (uint32_t)__builtin_amdgcn_readlane((int)sp.z, l),
                                           (uint32_t)__builtin_amdgcn_readlane((int)sp.w, l)));
-        if (a.tobs) {  // (the row's reads first, then the stores: one LDS round trip, not one per 64 values)
-          float* t = a.tobs + el * g.D;
-          if constexpr (PE_DONE_BATCH && DB) {
-            float tv[KD];
+        if constexpr (kOneWait) {
+          // loads first (the record above, the info rows, the terminal obs out of the
+          // tile), one wait, then every store
+          if (st.cur) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the commit's rows landed
+          const bool iload = a.tinfo && !info_iw && !stage_info;
+          Row4<MAXW> ir{0ull, 0ull, 0ull, 0ull};
+          if (iload) ir = coop_info_rows<MAXW>(st, g, el, lane);
+          float tv[KD];
 #pragma unroll
-            for (int j = 0; j < KD; ++j) tv[j] = lane + 64 * j < g.D ? tval(orow, lane + 64 * j) : 0.0f;
+          for (int j = 0; j < KD; ++j) tv[j] = a.tobs && lane + 64 * j < g.D ? tval(orow, lane + 64 * j) : 0.0f;
+          __builtin_amdgcn_s_waitcnt(0x0F70);  // (tracked: no later wait for these loads; stage: the DMA)
+          PE_DSTAMP(1);
+          if (a.tinfo && !info_iw) {
+            if (stage_info)
+              coop_info_store<MAXW, kLT>(st, g,
+                                    pf_stage_rows<MAXW>(reinterpret_cast<const uint64_t*>(
+                                                            stage + 4 + 4 * pf_grid_units(g.G, g.WPR) + a.pf.ostride / 4),
+                                                        g, lane),
+                                    sv, a.tinfo + el * PE_NINFO, lane, wf, ltab);
+            else
+              coop_info_store<MAXW, kLT>(st, g, ir, sv, a.tinfo + el * PE_NINFO, lane, wf, ltab);
+          }
+          PE_DSTAMP(2);
+          Row4<MAXW> rw;
+          Scal ns;
+          asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
+          const bool took = stage ? pf_stage_take<MAXW, OT, KD>(stage, g, (int)a.pf.ostride, sv.episode, rw, ns, orow, lane)
+                                  : (a.pf.scal && take(el, sv.episode, pl, rw, ns, orow));
+          if (took) {
+            ns = coop_apply_reset<MAXW, kLT>(st, g, el, ns, kp, rw, lane, ltab, true);
+          } else {
+            uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
+            ns = coop_reset_env<MAXW, kLT>(st, g, rl, el, sv.episode, kp, rw, lane, scr, ltab);
+            coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
+          }
+          PE_DSTAMP(3);
+          if (a.tobs) {
+            float* t = a.tobs + el * g.D;
 #pragma unroll
             for (int j = 0; j < KD; ++j)
               if (lane + 64 * j < g.D) t[lane + 64 * j] = tv[j];
-          } else {
-            for (int k2 = lane; k2 < g.D; k2 += 64) t[k2] = tval(orow, k2);
           }
-        }
-        // with the curriculum the commit stored this env's rows: they must land before
-        // the info reads them and the reset rewrites them
-        if (st.cur || (stage && !stage_reg)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (stage: the LDS-DMA landed)
-        PE_DSTAMP(1);
-        if (a.tinfo && !info_iw) {  // (register-staged info rows: the info wave's)
-          if (stage_info)  // the env's rows came with the record
-            coop_info_store<MAXW>(st, g,
-                                  pf_stage_rows<MAXW>(reinterpret_cast<const uint64_t*>(
-                                                          stage + 4 + 4 * pf_grid_units(g.G, g.WPR) + a.pf.ostride / 4),
-                                                      g, lane),
-                                  sv, a.tinfo + el * PE_NINFO, lane, wf, ltab);
-          else
-            coop_write_info<MAXW>(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, wf, ltab);
-        }
-        PE_DSTAMP(2);
-        Row4<MAXW> rw;
-        Scal ns;
-        asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
-        const bool took = stage ? pf_stage_take<MAXW, OT, PE_DONE_BATCH && DB ? KD : 0>(stage, g, (int)a.pf.ostride, sv.episode,
-                                                                                  rw, ns, orow, lane)
-                                : (a.pf.scal && take(el, sv.episode, pl, rw, ns, orow));
-        if (took) {
-          ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane, ltab, true);
+          if (a.pf.scal && lane == 0) a.pf.flag[el] = 1;  // its next map goes into the next generating batch
+          PE_DSTAMP(4);
+          if (done) {  // lane l: program order after its commit stores
+            s = ns;
+            st.ep_ret[e] = 0.0;
+            st.scal[e] = pack(s);
+          }
+          PE_DSTAMP(5);
         } else {
-          uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
-          ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane, scr, ltab);
-          coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
+          if (a.tobs) {  // (the row's reads first, then the stores: one LDS round trip, not one per 64 values)
+            float* t = a.tobs + el * g.D;
+            if constexpr (PE_DONE_BATCH && DB) {
+              float tv[KD];
+#pragma unroll
+              for (int j = 0; j < KD; ++j) tv[j] = lane + 64 * j < g.D ? tval(orow, lane + 64 * j) : 0.0f;
+#pragma unroll
+              for (int j = 0; j < KD; ++j)
+                if (lane + 64 * j < g.D) t[lane + 64 * j] = tv[j];
+            } else {
+              for (int k2 = lane; k2 < g.D; k2 += 64) t[k2] = tval(orow, k2);
+            }
+          }
+          // with the curriculum the commit stored this env's rows: they must land before
+          // the info reads them and the reset rewrites them
+          if (st.cur || (stage && !stage_reg)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (stage: the LDS-DMA landed)
+          PE_DSTAMP(1);
+          if (a.tinfo && !info_iw) {  // (register-staged info rows: the info wave's)
+            if (stage_info)  // the env's rows came with the record
+              coop_info_store<MAXW, kLT>(st, g,
+                                    pf_stage_rows<MAXW>(reinterpret_cast<const uint64_t*>(
+                                                            stage + 4 + 4 * pf_grid_units(g.G, g.WPR) + a.pf.ostride / 4),
+                                                        g, lane),
+                                    sv, a.tinfo + el * PE_NINFO, lane, wf, ltab);
+            else
+              coop_write_info<MAXW, kLT>(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, wf, ltab);
+          }
+          PE_DSTAMP(2);
+          Row4<MAXW> rw;
+          Scal ns;
+          asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
+          const bool took = stage ? pf_stage_take<MAXW, OT, PE_DONE_BATCH && DB ? KD : 0>(stage, g, (int)a.pf.ostride, sv.episode,
+                                                                                    rw, ns, orow, lane)
+                                  : (a.pf.scal && take(el, sv.episode, pl, rw, ns, orow));
+          if (took) {
+            ns = coop_apply_reset<MAXW, kLT>(st, g, el, ns, kp, rw, lane, ltab, true);
+          } else {
+            uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
+            ns = coop_reset_env<MAXW, kLT>(st, g, rl, el, sv.episode, kp, rw, lane, scr, ltab);
+            coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
+          }
+          PE_DSTAMP(3);
+          if (a.pf.scal && lane == 0) a.pf.flag[el] = 1;  // its next map goes into the next generating batch
+          PE_DSTAMP(4);
+          if (done) {  // lane l: program order after its commit stores
+            s = ns;
+            st.ep_ret[e] = 0.0;
+            st.scal[e] = pack(s);
+          }
+          PE_DSTAMP(5);
         }
-        PE_DSTAMP(3);
-        if (a.pf.scal && lane == 0) a.pf.flag[el] = 1;  // its next map goes into the next generating batch
-        PE_DSTAMP(4);
-        if (done) {  // lane l: program order after its commit stores
-          s = ns;
-          st.ep_ret[e] = 0.0;
-          st.scal[e] = pack(s);
-        }
-        PE_DSTAMP(5);
       }
     } else if (kIW && a.tinfo && wv == kQuadInfoWave && el_info_hit(e_info, e0, smem)) {
       // the terminal info of the early-record env (_get_info, plantos_env.py:317-336) by
@@ -846,7 +910,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
                                    (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(pk[2])),
                                    (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(pk[3])));
       const int wf = __builtin_amdgcn_readfirstlane(__float_as_int(pk[4]));
-      coop_info_store<MAXW>(st, g, *early_rows, unpack(spk), a.tinfo + e_info * PE_NINFO, lane, wf, ltab);
+      coop_info_store<MAXW, kLT>(st, g, *early_rows, unpack(spk), a.tinfo + e_info * PE_NINFO, lane, wf, ltab);
     } else if (info_iw && a.tinfo && wv == kQuadInfoWave) {
       // the terminal info of the staged env (the block's one done env: its truncation was
       // predicted) by the info wave from its rows register-staged in round 2 and its
@@ -859,7 +923,7 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
                                    (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(pk[2])),
                                    (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(pk[3])));
       const int wf = __builtin_amdgcn_readfirstlane(__float_as_int(pk[4]));
-      coop_info_store<MAXW>(st, g,
+      coop_info_store<MAXW, kLT>(st, g,
                             pf_stage_rows<MAXW>(reinterpret_cast<const uint64_t*>(
                                                     stage + 4 + 4 * pf_grid_units(g.G, g.WPR) + a.pf.ostride / 4),
                                                 g, lane),
@@ -909,6 +973,53 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
         if (k % NWv != wv) continue;
         const int64_t el = e0 + l;
         OT* orow = rows + l * g.D;
+        if constexpr (kOneWait) {
+          // loads first (the record, the info rows, the terminal obs), one wait, then
+          // every store (as the single-done path)
+          const uint4 sl = make_uint4((uint32_t)__builtin_amdgcn_readfirstlane((int)stage[5 * l]),
+                                      (uint32_t)__builtin_amdgcn_readfirstlane((int)stage[5 * l + 1]),
+                                      (uint32_t)__builtin_amdgcn_readfirstlane((int)stage[5 * l + 2]),
+                                      (uint32_t)__builtin_amdgcn_readfirstlane((int)stage[5 * l + 3]));
+          const int kw = __builtin_amdgcn_readfirstlane((int)stage[5 * l + 4]);
+          const bool kp = (kw & 1) != 0;
+          const Scal sv = unpack(sl);
+          const bool eh = KD <= 2 && early != nullptr && el == e_early;
+          const bool erows = eh && (!kIW || e_info == el);  // (as below)
+          PfLoad<MAXW, KD> pl;
+          if (a.pf.scal && !eh) coop_load_prefetched<MAXW, KD, OT>(a.pf, g, el, pl, lane);
+          Row4<MAXW> ir{0ull, 0ull, 0ull, 0ull};
+          if (a.tinfo && !erows) ir = coop_info_rows<MAXW>(st, g, el, lane);
+          float tv[KD];
+#pragma unroll
+          for (int j = 0; j < KD; ++j) tv[j] = a.tobs && lane + 64 * j < g.D ? tval(orow, lane + 64 * j) : 0.0f;
+          __builtin_amdgcn_s_waitcnt(0x0F70);
+          if (a.tinfo) coop_info_store<MAXW, kLT>(st, g, erows ? *early_rows : ir, sv, a.tinfo + el * PE_NINFO, lane, kw >> 1, ltab);
+          Row4<MAXW> rw;
+          Scal ns;
+          asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
+          if (a.pf.scal && take(el, sv.episode, eh ? *early : pl, rw, ns, orow)) {
+            ns = coop_apply_reset<MAXW, kLT>(st, g, el, ns, kp, rw, lane, ltab, true);
+          } else {
+            uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
+            ns = coop_reset_env<MAXW, kLT>(st, g, rl, el, sv.episode, kp, rw, lane, scr, ltab);
+            coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
+          }
+          if (a.tobs) {
+            float* t = a.tobs + el * g.D;
+#pragma unroll
+            for (int j = 0; j < KD; ++j)
+              if (lane + 64 * j < g.D) t[lane + 64 * j] = tv[j];
+          }
+          if (a.pf.scal && lane == 0) a.pf.flag[el] = 1;  // its next map goes into the next generating batch
+          const uint4 np = pack(ns);
+          if (lane == 0) {
+            stage[5 * l] = np.x;
+            stage[5 * l + 1] = np.y;
+            stage[5 * l + 2] = np.z;
+            stage[5 * l + 3] = np.w;
+          }
+          continue;
+        }
         if (a.tobs) {  // (the row's reads first, then the stores: one LDS round trip, not one per 64 values)
           float* t = a.tobs + el * g.D;
           if constexpr (PE_DONE_BATCH && DB) {
@@ -938,18 +1049,18 @@ __device__ __forceinline__ uint4 quad_done_path(const void* ka, int tile_off, in
           // (with the info wave the single early env's rows are that wave's, not this one's;
           // kEarly2's waves hold their env's rows themselves: e_info == e_early)
           if (eh && (!kIW || e_info == el))
-            coop_info_store<MAXW>(st, g, *early_rows, sv, a.tinfo + el * PE_NINFO, lane, kw >> 1, ltab);
+            coop_info_store<MAXW, kLT>(st, g, *early_rows, sv, a.tinfo + el * PE_NINFO, lane, kw >> 1, ltab);
           else
-            coop_write_info<MAXW>(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, kw >> 1, ltab);
+            coop_write_info<MAXW, kLT>(st, g, el, sv, a.tinfo + el * PE_NINFO, lane, kw >> 1, ltab);
         }
         Row4<MAXW> rw;
         Scal ns;
         asm volatile("" ::: "memory");  // terminal obs read out of the row before the fresh one goes in
         if (a.pf.scal && take(el, sv.episode, eh ? *early : pl, rw, ns, orow)) {
-          ns = coop_apply_reset<MAXW>(st, g, el, ns, kp, rw, lane, ltab, true);
+          ns = coop_apply_reset<MAXW, kLT>(st, g, el, ns, kp, rw, lane, ltab, true);
         } else {
           uint64_t* scr = reinterpret_cast<uint64_t*>(lrow) + 162 + wv * coop_scratch_words(g.G, g.WPR);
-          ns = coop_reset_env<MAXW>(st, g, rl, el, sv.episode, kp, rw, lane, scr, ltab);
+          ns = coop_reset_env<MAXW, kLT>(st, g, rl, el, sv.episode, kp, rw, lane, scr, ltab);
           coop_fresh_obs<MAXW>(g, rw, ns, orow, tdist, tpos, tvis, st.ldx, st.ldy, lane);
         }
         if (a.pf.scal && lane == 0) a.pf.flag[el] = 1;  // its next map goes into the next generating batch
@@ -2497,7 +2608,7 @@ __global__ __launch_bounds__(256) void pe_prefetch_kernel(StepArgs a, int all) {
     }
     // the new episode's fresh visit rows into its slot -- the env's idle one (episode
     // ep + 1 vs the running ep): the step that takes this record stores no visit row
-    coop_fresh_visits(a.st, g, e, s, lane, reinterpret_cast<const Tables*>(smem));
+    coop_fresh_visits<true>(a.st, g, e, s, lane, reinterpret_cast<const Tables*>(smem));
     if constexpr (BT)
       coop_fresh_obs<MAXW>(g, rw, s, reinterpret_cast<uint8_t*>(pf_obs_row(pf, e)), smem, smem + 72, smem + 328,
                            a.st.ldx, a.st.ldy, lane);
