@@ -557,6 +557,29 @@ def selftest_rank(args, world, rank):
         dist.destroy_process_group()
 
 
+WAIT_FLAGS = {"spin": 1, "yield": 2, "blocking": 4}  # hipDeviceSchedule*
+
+
+def set_wait_policy(torch, local):
+    """How the host waits for the GPU's completions (the window's closing synchronize):
+    PLANTOS_WAIT=auto (HIP's default, untouched) | spin | yield | blocking
+    (hipSetDeviceFlags on this rank's device, before anything else initialises it) |
+    poll (HSA_ENABLE_INTERRUPT=0: completion signals polled, not interrupt-driven).
+    Returns the policy applied."""
+    pol = os.environ.get("PLANTOS_WAIT", "auto")
+    if pol == "poll":
+        os.environ["HSA_ENABLE_INTERRUPT"] = "0"
+    elif pol in WAIT_FLAGS:
+        import ctypes
+        # the HIP runtime torch loaded (its own copy; the step library binds the same one)
+        hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+        if hip.hipSetDevice(local) != 0 or hip.hipSetDeviceFlags(WAIT_FLAGS[pol]) != 0:
+            raise SystemExit(f"bench.py: hipSetDeviceFlags({pol}) failed")
+    elif pol != "auto":
+        raise SystemExit(f"bench.py: PLANTOS_WAIT={pol}: auto | spin | yield | blocking | poll")
+    return pol
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -572,6 +595,7 @@ def main():
         return
 
     import torch
+    wait_policy = set_wait_policy(torch, local)
     dist = None
     nccl_version = None
     # a process group whenever a launcher started this process (WORLD_SIZE set) -- also
@@ -732,7 +756,8 @@ def main():
                        "parallelism": f"env-shard x{world} (independent replicas; RCCL gather leg: 'gather')",
                        "kernel": b.kernel_name,
                        "launch": launch_label(K, chunk) + (f" (warm-up: one {args.warmup}-step graph)"
-                                                           if K <= DIRECT_MAX and chunk and args.warmup > 0 else "")},
+                                                           if K <= DIRECT_MAX and chunk and args.warmup > 0 else ""),
+                       "host_wait": wait_policy},
             "resets_in_window": resets,
             "lib_sha": sha,
         }
