@@ -660,13 +660,24 @@ def main():
     # of a process pays more than later ones, so the window's is not the first
     # (profiles/r4aa_drv_ab.jsonl: 11.2 us per step median vs 12.1 with direct warm-up steps)
     wgraph = capture(args.warmup) if chunk and K <= DIRECT_MAX and args.warmup > 0 else None
+    # the auto-reset counters are read before the warm-up (PLANTOS_EP0=warmup, the default) and
+    # the line counts the resets of warm-up + window: read between the warm-up and the window
+    # (PLANTOS_EP0=window, exact window count) the state read -- a kernel, a copy, a host sync --
+    # costs a driver-shaped 20-step window ~1 us per step (profiles/r6/window_probe_r6v.jsonl)
+    ep_at = os.environ.get("PLANTOS_EP0", "warmup")
+    if ep_at not in ("warmup", "window"):
+        raise SystemExit(f"bench.py: PLANTOS_EP0={ep_at}: warmup | window")
+    if ep_at == "warmup":
+        ep0 = episodes(b)
+        torch.cuda.synchronize()
     if wgraph is not None:
         wgraph.replay()
     else:
         for t in range(args.warmup):
             one_step(t)
     torch.cuda.synchronize()
-    ep0 = episodes(b)
+    if ep_at == "window":
+        ep0 = episodes(b)
     elapsed, kern_ms = timed(torch, dist, device, K, one_step, chunk, graph)
     b.raise_on_errors()
     resets = resets_since(torch, dist, b, ep0)
@@ -758,7 +769,7 @@ def main():
                        "launch": launch_label(K, chunk) + (f" (warm-up: one {args.warmup}-step graph)"
                                                            if K <= DIRECT_MAX and chunk and args.warmup > 0 else ""),
                        "host_wait": wait_policy},
-            "resets_in_window": resets,
+            ("resets_in_window" if ep_at == "window" else "resets_in_warmup_and_window"): resets,
             "lib_sha": sha,
         }
         # roofline of the step kernel: algorithmic bytes x envs / its average launch

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """One driver-shaped window (20 steps after a 5-step warm-up graph) of the headline step per
 process, with bench.py's preamble switched piece by piece:
-  python tools/window_probe.py [upload=0|1] [episodes=0|1] [idle_ms=0]
+  python tools/window_probe.py [upload=0|1] [episodes=0|1] [episodes_before=0|1] [idle_ms=0]
 prints one JSON line (wall and HIP-event us per step of the first replay of the 20-step graph)."""
 import json
 import os
@@ -16,6 +16,7 @@ sys.path.insert(0, REPO)
 def main():
     opt = dict(a.split("=") for a in sys.argv[1:])
     upload, eps, idle_ms = int(opt.get("upload", 1)), int(opt.get("episodes", 1)), float(opt.get("idle_ms", 0))
+    eps_before = int(opt.get("episodes_before", 0))  # the counter read before the warm-up instead
     import torch
     import bench
     from plantos_amd import PlantOSBatch
@@ -39,6 +40,9 @@ def main():
 
     g20 = capture(K)
     g5 = capture(W)
+    if eps_before:
+        bench.episodes(b)
+        torch.cuda.synchronize()
     g5.replay()
     torch.cuda.synchronize()
     if eps:
@@ -54,7 +58,7 @@ def main():
     ev1.record(stream)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    print(json.dumps({"upload": upload, "episodes": eps, "idle_ms": idle_ms, "wall_us_per_step": wall / K * 1e6,
+    print(json.dumps({"upload": upload, "episodes": eps, "episodes_before": eps_before, "idle_ms": idle_ms, "wall_us_per_step": wall / K * 1e6,
                       "events_us_per_step": ev0.elapsed_time(ev1) / K * 1e3}), flush=True)
 
 
