@@ -301,7 +301,7 @@ def timed(torch, dist, device, K, one_step, chunk, graph, finish=None):
             elapsed = float(t[0])
         return elapsed, elapsed / K * 1e3
     if dist:
-        dist.barrier()
+        dist.barrier(group=BARRIER_GROUP)
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(device)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -323,7 +323,7 @@ def timed(torch, dist, device, K, one_step, chunk, graph, finish=None):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0  # this rank's K steps; the job's time is the max over ranks
     if dist:
-        dist.barrier()
+        dist.barrier(group=BARRIER_GROUP)
         torch.cuda.synchronize()
     kern_ms = ev0.elapsed_time(ev1) / K
     if dist:
@@ -558,6 +558,8 @@ def selftest_rank(args, world, rank):
 
 
 WAIT_FLAGS = {"spin": 1, "yield": 2, "blocking": 4}  # hipDeviceSchedule*
+# the process group of the barriers around the timed windows (main: PLANTOS_BARRIER)
+BARRIER_GROUP = None
 
 
 def set_wait_policy(torch, local):
@@ -607,6 +609,14 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"world size {dist.get_world_size()} != --gpus {args.gpus}")
+        # the windows' barriers: RCCL (PLANTOS_BARRIER=nccl, an all-reduce kernel on the GPU
+        # right before the window) or a host-side gloo group over the same rendezvous (gloo)
+        barrier_kind = os.environ.get("PLANTOS_BARRIER", "nccl")
+        if barrier_kind == "gloo":
+            global BARRIER_GROUP
+            BARRIER_GROUP = dist.new_group(backend="gloo")
+        elif barrier_kind != "nccl":
+            raise SystemExit(f"bench.py: PLANTOS_BARRIER={barrier_kind}: nccl | gloo")
         try:
             nccl_version = ".".join(str(v) for v in torch.cuda.nccl.version())
         except Exception:  # noqa: BLE001
@@ -768,7 +778,8 @@ def main():
                        "kernel": b.kernel_name,
                        "launch": launch_label(K, chunk) + (f" (warm-up: one {args.warmup}-step graph)"
                                                            if K <= DIRECT_MAX and chunk and args.warmup > 0 else ""),
-                       "host_wait": wait_policy},
+                       "host_wait": wait_policy,
+                       "barrier": (os.environ.get("PLANTOS_BARRIER", "nccl") if dist else None)},
             ("resets_in_window" if ep_at == "window" else "resets_in_warmup_and_window"): resets,
             "lib_sha": sha,
         }
